@@ -1,0 +1,156 @@
+/*
+ * vblade.h — C ABI of libvblade_hip.so, the MI355X (gfx950) block-sparse attention path of
+ * Video-BLADE. Plain pointers, sizes and strides; no framework types. Every device pointer is
+ * a HIP device address; `stream` is a hipStream_t (NULL = the null stream).
+ *
+ * Contract:
+ *   - the caller owns every buffer (inputs read-only, outputs fully overwritten); the library
+ *     never allocates, frees or synchronises, so every entry point is hipGraph-capturable;
+ *   - return 0 on success, a negative VB_ERR_* code otherwise; vb_last_error() holds the message
+ *     of the last failure on the calling thread; no C++ exception crosses the ABI;
+ *   - stateless and reentrant; all work is enqueued on `stream`.
+ *
+ * Tensor convention: "[B,H,L,D] strided" = element (b,h,l,d) at base + b*s[0] + h*s[1] + l*s[2] + d,
+ * strides in ELEMENTS, innermost (d) stride 1. Row-index arrays ("rows") map a position of the
+ * reordered (Gilbert) sequence to the row of the caller's tensor that holds it; NULL = identity.
+ */
+#ifndef VBLADE_H_
+#define VBLADE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VB_ABI_VERSION 1
+
+enum vb_status {
+  VB_OK = 0,
+  VB_ERR_INVALID = -1,     /* bad argument / shape */
+  VB_ERR_UNSUPPORTED = -2, /* valid for the reference op but not implemented (dropout, causal, streaming, head dim) */
+  VB_ERR_LAUNCH = -3       /* the HIP launch failed */
+};
+
+enum vb_dtype { VB_DTYPE_BF16 = 0, VB_DTYPE_F16 = 1 };
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* vb_last_error(void);
+int vb_abi_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Gilbert 3-D curve permutation (host). Replaces GilbertRearranger.__init__ /
+ * _gilbert3d_with_index + utils/gilbert3d.py:6-167
+ * (cogvideox/train/special_attentions_local/TrainRelated/cogvideo_blocksparseattn.py:112-140).
+ * perm_out[g] = x + width*(y + height*z) of the g-th curve point (length width*height*depth).
+ * ------------------------------------------------------------------------------------------ */
+int vb_gilbert3d_perm(int width, int height, int depth, int32_t* perm_out);
+
+/* ------------------------------------------------------------------------------------------
+ * Drop-in for block_sparse_attn_func forward (mit-han-lab/Block-Sparse-Attention) exactly as the
+ * reference calls it: cogvideo_blocksparseattn.py:316-320 (also :106-109 for the dense pooled
+ * call; wanx_blocksparseattn.py:301-305).
+ *   q/k/v_unpad   [total, H, D] contiguous, dtype `dtype`
+ *   cu_seqlens_*  int32 [batch+1] (device)
+ *   head_mask_type int32 [H] (device): 0 dense; m>0 block-sparse with base_blockmask head m-1,
+ *                 where every 1 is first renumbered 1,2,3,... in head order (the library's
+ *                 replace_ones_with_count); m<0 (streaming) -> that head's output is NaN.
+ *   streaming_info ignored (only used by streaming heads)
+ *   base_blockmask uint8/bool [batch, n_sparse, ceil(max_q/128), ceil(max_k/128)] contiguous
+ *   out_unpad     [total_q, H, D]; softmax_lse fp32 [batch, H, max_seqlen_q] (natural log)
+ *   p_dropout must be 0, is_causal/exact_streaming must be 0 (the reference's call) else
+ *   VB_ERR_UNSUPPORTED. softmax_scale <= 0 means head_dim^-1/2. `deterministic` is accepted
+ *   and ignored (the forward is deterministic).
+ * ------------------------------------------------------------------------------------------ */
+int vb_block_sparse_attn_fwd(const void* q_unpad, const void* k_unpad, const void* v_unpad,
+                             const int32_t* cu_seqlens_q, const int32_t* cu_seqlens_k,
+                             const int32_t* head_mask_type, const int32_t* streaming_info,
+                             const uint8_t* base_blockmask, int batch, int num_heads, int head_dim,
+                             int max_seqlen_q, int max_seqlen_k, float p_dropout, int deterministic,
+                             float softmax_scale, int is_causal, int exact_streaming, int dtype,
+                             void* out_unpad, float* softmax_lse, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Native strided block-sparse attention forward (the adaptive module's hot kernel). One softmax
+ * over the union of
+ *   (a) full-resolution keys of the 128x128 blocks kept by `block_mask` (NULL = all kept), and
+ *   (b) optionally, `Lkp` pooled keys kp/vp carrying an additive score bias `kp_log_bias`
+ *       (= ln sample_gap: the LSE combine of cogvideo_blocksparseattn.py:374-393 fused as one
+ *       softmax).
+ * Setting use_main=0 attends only to (b) (the reference's standard_attn, :106-109).
+ * q rows are read at q_rows[g] and out/lse written at q_rows[g] (g = reordered position), so
+ * the Gilbert reorder and its inverse (:141-161) cost no separate pass; k/v rows read at kv_rows[g].
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vb_attn_args {
+  const void* q; const void* k; const void* v;
+  int64_t q_stride[3]; int64_t k_stride[3]; int64_t v_stride[3];
+  const int32_t* q_rows;  /* [Lq] or NULL */
+  const int32_t* kv_rows; /* [Lk] or NULL */
+  int use_main;           /* attend to the block-masked full-resolution keys */
+  const uint8_t* block_mask; int64_t mask_stride[3]; /* [B,H,ceil(Lq/128),ceil(Lk/128)] or NULL */
+  const void* kp; const void* vp;                     /* pooled keys [B,H,Lkp,D] strided or NULL */
+  int64_t kp_stride[3]; int64_t vp_stride[3];
+  int Lkp; float kp_log_bias;
+  void* out; int64_t out_stride[3];
+  float* lse;             /* [B,H,Lq] fp32 natural-log LSE (written at q_rows) or NULL */
+  int B, H, Lq, Lk, D;
+  float scale;            /* <= 0 -> D^-1/2 */
+  int dtype;
+} vb_attn_args;
+int vb_attn_fwd(const vb_attn_args* args, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused mask predictor (a3+a4+a5): efficient_attn_with_pooling + attn_with_pooling (Triton,
+ * attn_pooling_kernel.py:17-255) + transfer_attn_to_mask(mode="energy")
+ * (cogvideo_blocksparseattn.py:57-82, 177-249; wanx_blocksparseattn.py:162-233).
+ * For each (b,h): the reordered sequence (rows, replicate-padded to a multiple of `block`) is
+ * sampled at the `num_keep` offsets q_off[b,h,:] / k_off[b,h,:] of every block; pooled scores
+ * Po [nb,nb] (storage dtype, row-normalised) are written to `po` and the energy rule
+ * (threshold, min/max kept blocks, last `force_tail` rows/cols forced) writes `mask` [B,H,nb,nb].
+ * Ties between equal Po values are kept lowest-block-first. `mask_count` (nullable) receives
+ * an atomic add of the number of kept blocks (device-side sparsity statistic, no host sync).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vb_predict_args {
+  const void* q; const void* k;
+  int64_t q_stride[3]; int64_t k_stride[3];
+  const int32_t* rows;     /* [L] reordered -> caller row, or NULL */
+  const int32_t* q_off;    /* [B,H,num_keep] int32 in [0,block) */
+  const int32_t* k_off;
+  int B, H, L, D, block, num_keep;
+  float scale;             /* <= 0 -> D^-1/2 */
+  float energy_threshold;
+  int min_keep, max_keep, force_tail;
+  void* po;                /* [B,H,nb,nb] storage dtype, contiguous */
+  uint8_t* mask;           /* [B,H,nb,nb] contiguous */
+  unsigned long long* mask_count; /* nullable */
+  int dtype;
+} vb_predict_args;
+int vb_mask_predict(const vb_predict_args* args, void* stream);
+
+/* Energy rule alone on given scores (transfer_attn_to_mask, mode="energy"):
+ * po [B,H,nr,nc] contiguous storage dtype -> mask [B,H,nr,nc]. */
+int vb_energy_mask(const void* po, int B, int H, int nr, int nc, float energy_threshold,
+                   int min_keep, int max_keep, int force_tail, int dtype, uint8_t* mask,
+                   unsigned long long* mask_count, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Mean pooling of K and V over `gap` consecutive reordered tokens with replicate padding
+ * (simple_pooling, cogvideo_blocksparseattn.py:83-88): kp/vp [B,H,ceil(L/gap),D] contiguous.
+ * ------------------------------------------------------------------------------------------ */
+int vb_pool_kv(const void* k, const void* v, const int64_t* k_stride, const int64_t* v_stride,
+               const int32_t* rows, int B, int H, int L, int D, int gap, int dtype, void* kp,
+               void* vp, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Reference-faithful LSE combine (cogvideo_blocksparseattn.py:374-393, each eager op rounded to
+ * the storage dtype): out = out1*a + out2*(1-a), a = e1/(e1+e2) from lse1 and lse2 + ln(gap).
+ * All tensors [B,H,L,(D)] contiguous; alpha (nullable) receives a as fp32 [B,H,L].
+ * ------------------------------------------------------------------------------------------ */
+int vb_lse_combine(const void* out1, const float* lse1, const void* out2, const float* lse2,
+                   int B, int H, int L, int D, float gap, int dtype, void* out, float* alpha,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VBLADE_H_ */

@@ -1,0 +1,127 @@
+"""CPU: the C ABI library loads, exports every symbol include/vblade.h declares, its ctypes
+struct layouts match the C header (compiled with gcc), host-side entry points behave, and the
+argument validation returns the documented error codes without touching a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+HEADER = os.path.join(ROOT, "include", "vblade.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vb_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from vblade import _lib
+    return _lib.load()
+
+
+def test_every_declared_symbol_is_exported_and_bound(lib):
+    from vblade import _lib
+    names = _declared_functions()
+    assert names, "no functions parsed from vblade.h"
+    for n in names:
+        assert hasattr(lib, n), f"{n} missing from libvblade_hip.so"
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
+    assert set(_lib.SIGNATURES) == set(names)
+
+
+def test_abi_version(lib):
+    assert lib.vb_abi_version() == 1
+
+
+def test_struct_layouts_match_header():
+    """sizeof/offsetof of vb_attn_args and vb_predict_args from gcc == the ctypes mirrors."""
+    from vblade._lib import AttnArgs, PredictArgs
+    fields = {"vb_attn_args": [f[0] for f in AttnArgs._fields_],
+              "vb_predict_args": [f[0] for f in PredictArgs._fields_]}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for st, fl in fields.items():
+        lines.append(f'printf("{st} %zu\\n", sizeof({st}));')
+        for f in fl:
+            lines.append(f'printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    lines.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write("\n".join(lines))
+        exe = os.path.join(d, "l")
+        subprocess.check_call(["gcc", "-std=c99", c, "-o", exe])
+        out = subprocess.check_output([exe]).decode().split("\n")
+    got = dict(line.split() for line in out if line)
+    for st, cls in (("vb_attn_args", AttnArgs), ("vb_predict_args", PredictArgs)):
+        assert int(got[st]) == ctypes.sizeof(cls), st
+        for f in fields[st]:
+            assert int(got[f"{st}.{f}"]) == getattr(cls, f).offset, f"{st}.{f}"
+
+
+def test_gilbert_perm_host_entry_matches_reference_fixture(lib):
+    from vblade import ops
+    z = np.load(os.path.join(GOLDEN, "gilbert_perms.npz"))
+    for key in z.files:
+        w, h, d = map(int, key.split("_")[1].split("x"))
+        assert np.array_equal(ops.gilbert_perm(w, h, d), z[key]), key
+
+
+def test_invalid_arguments_return_codes_without_gpu(lib):
+    from vblade import _lib
+    buf = np.zeros(8, dtype=np.int32)
+    assert lib.vb_gilbert3d_perm(0, 2, 2, buf.ctypes.data) == _lib.VB_ERR_INVALID
+    assert b"positive" in lib.vb_last_error()
+    # dropout is rejected before any device work
+    rc = lib.vb_block_sparse_attn_fwd(1, 1, 1, 1, 1, None, None, None, 1, 1, 64, 128, 128,
+                                      0.1, 1, 0.0, 0, 0, 0, 1, 1, None)
+    assert rc == _lib.VB_ERR_UNSUPPORTED and b"dropout" in lib.vb_last_error()
+    rc = lib.vb_block_sparse_attn_fwd(1, 1, 1, 1, 1, None, None, None, 1, 1, 64, 128, 128,
+                                      0.0, 1, 0.0, 1, 0, 0, 1, 1, None)
+    assert rc == _lib.VB_ERR_UNSUPPORTED
+    a = _lib.AttnArgs()
+    assert lib.vb_attn_fwd(ctypes.byref(a), None) == _lib.VB_ERR_INVALID
+    p = _lib.PredictArgs()
+    assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
+    assert lib.vb_energy_mask(None, 1, 1, 1, 1, 0.95, 1, 1, 0, 0, None, None, None) == _lib.VB_ERR_INVALID
+    assert lib.vb_pool_kv(None, None, None, None, None, 1, 1, 1, 64, 15, 0, None, None, None) == _lib.VB_ERR_INVALID
+    assert lib.vb_lse_combine(None, None, None, None, 1, 1, 1, 64, 15.0, 0, None, None, None) == _lib.VB_ERR_INVALID
+
+
+def test_ops_refuse_cpu_tensors():
+    """The product path has no CPU fallback: CPU tensors raise."""
+    import torch
+    from vblade import ops
+    q = torch.zeros(1, 1, 128, 64, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="HIP"):
+        ops.attention_fwd(q, q, q)
+
+
+def test_module_config_and_retain_counts():
+    import vblade
+    from vblade.attention import retain_counts
+    m = vblade.AdaptiveBlockSparseAttn("cog")
+    assert m.gilbert_rearranger.seq_len == 17776 and m.force_tail == 2 and m.sample_gap == 15
+    w = vblade.AdaptiveBlockSparseAttn("wan")
+    assert w.gilbert_rearranger.seq_len == 32760 and w.force_tail == 0 and w.sample_gap == 30
+    assert retain_counts(139, 0.05, 0.1, "cog") == (6, 13)
+    assert retain_counts(256, 0.05, 0.17, "wan") == (12, 43)
+    rows = m.gilbert_rearranger.rows.long()
+    assert sorted(rows.tolist()) == list(range(17776))
+    assert rows[-226:].tolist() == list(range(226))  # text tail, in order
+
+
+def test_gilbert_rearranger_round_trip_cpu():
+    import torch
+    import vblade
+    g = vblade.GilbertRearranger(8, 6, 4, text_length=10)
+    x = torch.randn(2, 3, 8 * 6 * 4 + 10, 16)
+    q, k, v = g.rearrange(x, x, x)
+    assert torch.equal(q[..., -10:, :], x[..., :10, :])
+    assert torch.equal(g.reversed_rearrange(q), x)

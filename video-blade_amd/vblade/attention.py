@@ -1,0 +1,220 @@
+"""Adaptive block-sparse attention module — the ``attn.inner_attention(q, k, v)`` surface.
+
+Mirrors ``AdaptiveBlockSparseAttnTrain`` (cogvideox/train/special_attentions_local/TrainRelated/
+cogvideo_blocksparseattn.py:398-427; wanx_blocksparseattn.py:375-409) and its helpers
+(``adaptive_block_sparse_attn`` :327-394, ``GilbertRearranger`` :110-161,
+``transfer_attn_to_mask`` :177-249, ``simple_pooling`` :83-88), with the module-level globals
+(:9-16) as constructor arguments. Every tensor op of the hot path runs in libvblade_hip.so:
+
+  forward (inference, the 8-step samplers):
+    1. vb_mask_predict  — sampled pooled scores + energy top-k -> block mask (Gilbert order)
+    2. vb_pool_kv       — mean-pooled K/V over `sample_gap` reordered tokens
+    3. vb_attn_fwd      — ONE softmax over kept full-res keys ∪ pooled keys (+ln gap bias):
+                          the reference's two attention calls + LSE combine, fused; q/k/v rows
+                          gathered and out rows scattered through the Gilbert index (no copies)
+  training (grad required) keeps the reference's two-branch structure so the backward has the
+  reference's semantics (LSE/alpha detached): see ``ops_autograd.AdaptiveSplitAttention``.
+
+Only the tiny RNG draw of the sampling offsets (torch.rand + topk over [B,H,1,128], exactly as
+cogvideo_blocksparseattn.py:45-46 so the RNG stream matches the reference) stays in PyTorch.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+
+VARIANT_DEFAULTS = {
+    # cogvideo_blocksparseattn.py:9-16
+    "cog": dict(use_rearrange=True, max_retain_ratio=0.1, min_retain_ratio=0.05, width=45,
+                height=30, depth=13, sample_gap=15, text_length=226, force_tail=2, log_every=800),
+    # wanx_blocksparseattn.py:9-16 (+ no forced rows/cols, print every 200 calls :400)
+    "wan": dict(use_rearrange=True, max_retain_ratio=0.17, min_retain_ratio=0.05, width=52,
+                height=30, depth=21, sample_gap=30, text_length=0, force_tail=0, log_every=200),
+}
+
+
+def retain_counts(nb: int, min_ratio: float, max_ratio: float, variant: str):
+    """Kept-block clamp bounds. cog: (seq * fp32 ratio tensor).to(int) clamped >= 1
+    (cogvideo_blocksparseattn.py:230-231, 347-348); wan: max(1, int(seq * ratio)) (wanx :215-216)."""
+    if variant == "cog":
+        lo = int(np.float32(nb) * np.float32(min_ratio))
+        hi = int(np.float32(nb) * np.float32(max_ratio))
+    else:
+        lo, hi = int(nb * min_ratio), int(nb * max_ratio)
+    return max(1, lo), max(1, hi)
+
+
+def draw_sample_offsets(B: int, H: int, device, block: int = 128, num_keep: int = 32,
+                        generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """rand(B,H,1,block) -> topk(num_keep) offsets, shared by all blocks of a (b,h)
+    (random_sample_tokens, cogvideo_blocksparseattn.py:45-46). int32 [B,H,num_keep]."""
+    r = torch.rand(B, H, 1, block, device=device, generator=generator)
+    return torch.topk(r, num_keep, dim=3).indices[:, :, 0, :].to(torch.int32)
+
+
+class GilbertRearranger(nn.Module):
+    """Index maps of the Gilbert reorder (cogvideo_blocksparseattn.py:110-161; wanx :102-159).
+
+    ``rows[g]`` = caller row holding reordered position g. The attention kernels consume
+    ``rows`` directly; ``rearrange``/``reversed_rearrange`` are provided for API parity and
+    debugging (they materialise copies the fused path never makes)."""
+
+    def __init__(self, width: int, height: int, depth: int, text_length: int = 0):
+        super().__init__()
+        self.width, self.height, self.depth, self.text_length = width, height, depth, text_length
+        perm = ops.gilbert_perm(width, height, depth).astype(np.int64)
+        inv = np.empty_like(perm)
+        inv[perm] = np.arange(perm.size)
+        self.register_buffer("original_order2gilbert_order", torch.from_numpy(perm), persistent=False)
+        self.register_buffer("gilbert_order2original_order", torch.from_numpy(inv), persistent=False)
+        rows = np.concatenate([perm + text_length, np.arange(text_length)]).astype(np.int32)
+        self.register_buffer("rows", torch.from_numpy(rows), persistent=False)
+
+    @property
+    def seq_len(self) -> int:
+        return self.width * self.height * self.depth + self.text_length
+
+    def rearrange(self, q, k, v):
+        r = self.rows.to(q.device).long()
+        return q[..., r, :], k[..., r, :], v[..., r, :]
+
+    def reversed_rearrange(self, out):
+        r = self.rows.to(out.device).long()
+        res = torch.empty_like(out)
+        res[..., r, :] = out
+        return res
+
+
+class AdaptiveBlockSparseAttn(nn.Module):
+    """``inner_attention(q, k, v) -> out`` with q,k,v,out [B,H,L,D] bf16/fp16 on a HIP device.
+
+    variant: "cog" (CogVideoX-5B: text tail, forced last 2 block rows/cols) or "wan"
+    (Wan2.1-1.3B). Keyword arguments override the reference's module globals.
+    combine: "fused" (one softmax, inference default) or "reference" (two attention calls + the
+    reference's bf16 LSE combine, bit-for-bit structure of :366-393; always used under autograd).
+    """
+
+    def __init__(self, variant: str = "cog", *, combine: str = "fused", **overrides):
+        super().__init__()
+        if variant not in VARIANT_DEFAULTS:
+            raise ValueError(f"variant must be one of {list(VARIANT_DEFAULTS)}")
+        cfg = dict(VARIANT_DEFAULTS[variant])
+        unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep"}
+        if unknown:
+            raise TypeError(f"unknown options {sorted(unknown)}")
+        cfg.update(overrides)
+        self.variant = variant
+        self.combine = combine
+        self.use_rearrange = cfg["use_rearrange"]
+        self.max_retain_ratio = cfg["max_retain_ratio"]
+        self.min_retain_ratio = cfg["min_retain_ratio"]
+        self.sample_gap = int(cfg["sample_gap"])
+        self.text_length = int(cfg["text_length"])
+        self.force_tail = int(cfg["force_tail"])
+        self.energy_threshold = float(cfg.get("energy_threshold", 0.95))
+        self.block = int(cfg.get("block", 128))
+        self.num_keep = int(cfg.get("num_keep", 32))
+        if self.block != 128 or self.num_keep != 32:
+            raise ValueError("block=128 and num_keep=32 are the reference's (only) values")
+        self.log_every = int(cfg["log_every"])
+        self.gilbert_rearranger = GilbertRearranger(cfg["width"], cfg["height"], cfg["depth"],
+                                                    self.text_length)
+        # running sparsity statistic kept on the device (the reference's .item() per call, :415,
+        # is replaced by a device counter; read it through .sparsity)
+        self.sparsity_counter = 0
+        self._kept_slots = None
+        self._slot_totals = []
+        self.last_mask: Optional[torch.Tensor] = None
+
+    # -------------------------------------------------------------------------------- helpers
+    def _rows(self, device):
+        if not self.use_rearrange:
+            return None
+        r = self.gilbert_rearranger.rows
+        if r.device != device:
+            r = r.to(device)
+            self.gilbert_rearranger.rows = r
+        return r
+
+    def _count_slot(self, device):
+        if self._kept_slots is None or self._kept_slots.device != device:
+            self._kept_slots = torch.zeros(4096, dtype=torch.int64, device=device)
+            self._slot_totals = []
+        i = len(self._slot_totals) % self._kept_slots.numel()
+        if i == 0 and self._slot_totals:
+            self._fold_slots()
+            i = 0
+        return self._kept_slots[i:i + 1]
+
+    def _fold_slots(self):
+        kept = self._kept_slots[:len(self._slot_totals)].double().cpu().numpy()
+        tot = np.asarray(self._slot_totals, dtype=np.float64)
+        self._folded = getattr(self, "_folded", 0.0) + float(np.sum(1.0 - kept / tot - 1.0 / self.sample_gap))
+        self._kept_slots.zero_()
+        self._slot_totals = []
+
+    @property
+    def sparsity(self) -> float:
+        """Average reported sparsity 1 - mean(mask) - 1/sample_gap over all calls (:394, :415).
+        Reading it synchronises once; the forward never does."""
+        if self.sparsity_counter == 0:
+            return 0.0
+        if self._slot_totals:
+            self._fold_slots()
+        return getattr(self, "_folded", 0.0) / self.sparsity_counter
+
+    # -------------------------------------------------------------------------------- forward
+    def predict_mask(self, q, k, q_off=None, k_off=None, count=None):
+        """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores."""
+        B, H, L, D = q.shape
+        if q_off is None:
+            q_off = draw_sample_offsets(B, H, q.device)
+        if k_off is None:
+            k_off = draw_sample_offsets(B, H, q.device)
+        nb = (L + self.block - 1) // self.block
+        lo, hi = retain_counts(nb, self.min_retain_ratio, self.max_retain_ratio, self.variant)
+        po, mask = ops.mask_predict(q, k, q_off, k_off, rows=self._rows(q.device),
+                                    energy_threshold=self.energy_threshold, min_keep=lo,
+                                    max_keep=hi, force_tail=self.force_tail, mask_count=count)
+        return po, mask
+
+    def forward(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *,
+                q_off: Optional[torch.Tensor] = None, k_off: Optional[torch.Tensor] = None,
+                block_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, H, L, D = q.shape
+        if self.use_rearrange and L != self.gilbert_rearranger.seq_len:
+            raise ValueError(f"sequence length {L} != {self.gilbert_rearranger.seq_len} expected "
+                             f"by the Gilbert grid (width/height/depth/text_length)")
+        rows = self._rows(q.device)
+        nb = (L + self.block - 1) // self.block
+        count = self._count_slot(q.device)
+        if block_mask is None:
+            with torch.no_grad():
+                _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count)
+        else:
+            mask = block_mask.to(torch.uint8)
+            count.add_(mask.sum())
+        self._slot_totals.append(B * H * nb * nb)
+        self.sparsity_counter += 1
+        self.last_mask = mask
+        grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)
+        if grad or self.combine == "reference":
+            from .autograd import adaptive_split_attention
+            out = adaptive_split_attention(q, k, v, mask, rows, self.sample_gap)
+        else:
+            kp, vp = ops.pool_kv(k, v, self.sample_gap, rows)
+            out = ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kv_rows=rows, kp=kp,
+                                    vp=vp, kp_log_bias=math.log(self.sample_gap))
+        if self.log_every and self.sparsity_counter % self.log_every == 0:
+            print(f"sparsity: {self.sparsity}")
+        return out
+
+
+# reference-named alias (the patch functions install one shared instance on every block)
+AdaptiveBlockSparseAttnTrain = AdaptiveBlockSparseAttn

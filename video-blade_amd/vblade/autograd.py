@@ -1,0 +1,78 @@
+"""autograd.Function wrappers with the reference's gradient semantics.
+
+* ``block_sparse_attn_func`` — drop-in for mit-han-lab/Block-Sparse-Attention's function of the
+  same name as called at cogvideo_blocksparseattn.py:316-320 (differentiable in q, k, v; the
+  returned LSE carries no gradient, FlashAttention-2 convention).
+* ``adaptive_split_attention`` — adaptive_block_sparse_attn's two-branch form (:366-393): block-
+  sparse branch + pooled dense branch + bf16 LSE combine. Under autograd alpha is a constant
+  (both LSEs are detached), so dO1 = alpha*dO, dO2 = (1-alpha)*dO and each branch back-propagates
+  with its own output and LSE; pooled-branch K/V gradients flow back through the mean pool.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+class _BlockSparseAttnFunc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, cu_q, cu_k, head_mask_type, streaming_info, base_blockmask,
+                max_q, max_k, p_dropout, deterministic, softmax_scale, is_causal, exact_streaming):
+        out, lse = ops.block_sparse_attn_fwd(q, k, v, cu_q, cu_k, head_mask_type, streaming_info,
+                                             base_blockmask, max_q, max_k, p_dropout,
+                                             deterministic, softmax_scale, is_causal,
+                                             exact_streaming)
+        ctx.save_for_backward(q, k, v, out, lse, cu_q, cu_k, head_mask_type, base_blockmask)
+        ctx.meta = (max_q, max_k, softmax_scale)
+        ctx.mark_non_differentiable(lse)
+        return out, lse
+
+    @staticmethod
+    def backward(ctx, dout, _dlse):
+        from . import backward as bw
+        q, k, v, out, lse, cu_q, cu_k, hmt, mask = ctx.saved_tensors
+        max_q, max_k, scale = ctx.meta
+        dq, dk, dv = bw.block_sparse_attn_bwd(dout, q, k, v, out, lse, cu_q, cu_k, hmt, mask,
+                                              max_q, max_k, scale)
+        return (dq, dk, dv) + (None,) * 12
+
+
+def block_sparse_attn_func(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k, head_mask_type,
+                           streaming_info, base_blockmask, max_seqlen_q_, max_seqlen_k_, p_dropout,
+                           deterministic=False, softmax_scale=None, is_causal=False,
+                           exact_streaming=False, return_attn_probs=False):
+    """Same signature and return convention as the reference's external op."""
+    out, lse = _BlockSparseAttnFunc.apply(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k,
+                                          head_mask_type, streaming_info, base_blockmask,
+                                          max_seqlen_q_, max_seqlen_k_, p_dropout, deterministic,
+                                          softmax_scale, is_causal, exact_streaming)
+    if return_attn_probs:
+        return out, lse, None
+    return out
+
+
+class _AdaptiveSplitFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, mask, rows, gap):
+        out1, lse1 = ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kv_rows=rows,
+                                       need_lse=True)
+        kp, vp = ops.pool_kv(k, v, gap, rows)
+        out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
+                                       need_lse=True)
+        out, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
+        ctx.save_for_backward(q, k, v, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp)
+        ctx.gap = gap
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import backward as bw
+        q, k, v, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp = ctx.saved_tensors
+        dq, dk, dv = bw.adaptive_split_bwd(dout, q, k, v, mask, rows, out1, lse1, out2, lse2,
+                                           alpha, kp, vp, ctx.gap)
+        return dq, dk, dv, None, None, None
+
+
+def adaptive_split_attention(q, k, v, mask, rows, gap):
+    return _AdaptiveSplitFn.apply(q, k, v, mask, rows, gap)

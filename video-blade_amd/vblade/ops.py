@@ -1,0 +1,248 @@
+"""Torch-facing wrappers over the C ABI (include/vblade.h).
+
+PyTorch supplies device memory and the current HIP stream only; every byte of the hot path is
+computed by libvblade_hip.so. Calls on CPU tensors raise (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import AttnArgs, PredictArgs, check
+
+BLOCK = 128
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return _lib.VB_DTYPE_BF16
+    if t.dtype == torch.float16:
+        return _lib.VB_DTYPE_F16
+    raise TypeError(f"vblade: unsupported dtype {t.dtype} (bf16/fp16 only)")
+
+
+def _require_gpu(*ts: Optional[torch.Tensor]):
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("vblade: tensors must live on a HIP (cuda) device; there is no CPU path")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError("vblade: tensors on different devices")
+    return dev
+
+
+def _stream(dev) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _s3(t: torch.Tensor):
+    """(batch, head, row) element strides of a [B,H,L,D] tensor with unit d-stride."""
+    if t.stride(-1) != 1:
+        raise ValueError("vblade: last dimension must be contiguous")
+    return (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2))
+
+
+def _aligned_bhld(t: torch.Tensor) -> torch.Tensor:
+    """Return t if its strides/pointer satisfy the kernels' 16-byte rules, else a contiguous copy."""
+    if (t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:3]) and t.data_ptr() % 16 == 0):
+        return t
+    return t.contiguous()
+
+
+# ----------------------------------------------------------------------------------------------
+# Gilbert permutation
+# ----------------------------------------------------------------------------------------------
+def gilbert_perm(width: int, height: int, depth: int) -> np.ndarray:
+    """perm[g] = x + W*(y + H*z) of the g-th Gilbert point (vb_gilbert3d_perm, host C++)."""
+    n = width * height * depth
+    out = np.empty(n, dtype=np.int32)
+    check(_lib.load().vb_gilbert3d_perm(width, height, depth, out.ctypes.data), "vb_gilbert3d_perm")
+    return out
+
+
+def sequence_rows(width: int, height: int, depth: int, text_length: int) -> np.ndarray:
+    """Reordered position -> caller row: [video[perm] (+text offset), text] (CogVideoX puts the
+    text tail last, cogvideo_blocksparseattn.py:141-154; Wan has text_length 0)."""
+    perm = gilbert_perm(width, height, depth).astype(np.int64) + text_length
+    return np.concatenate([perm, np.arange(text_length)]).astype(np.int32)
+
+
+# ----------------------------------------------------------------------------------------------
+# attention forward
+# ----------------------------------------------------------------------------------------------
+def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.Tensor], *,
+                  block_mask: Optional[torch.Tensor] = None, q_rows: Optional[torch.Tensor] = None,
+                  kv_rows: Optional[torch.Tensor] = None, kp: Optional[torch.Tensor] = None,
+                  vp: Optional[torch.Tensor] = None, kp_log_bias: float = 0.0, use_main: bool = True,
+                  scale: Optional[float] = None, need_lse: bool = False,
+                  out: Optional[torch.Tensor] = None):
+    """vb_attn_fwd: softmax over (block-masked keys of k/v) ∪ (pooled keys kp/vp + bias).
+    q,k,v [B,H,L,D]; block_mask [B,H,ceil(Lq/128),ceil(Lk/128)] bool/uint8; rows int32.
+    Returns out [B,H,Lq,D] (and lse fp32 [B,H,Lq] when need_lse)."""
+    dev = _require_gpu(q, k, v, block_mask, q_rows, kv_rows, kp, vp)
+    q = _aligned_bhld(q)
+    B, H, Lq, D = q.shape
+    if use_main:
+        k, v = _aligned_bhld(k), _aligned_bhld(v)
+        Lk = k.shape[2]
+    else:
+        Lk = 0
+    if kp is not None:
+        kp, vp = _aligned_bhld(kp), _aligned_bhld(vp)
+    if out is None:
+        out = torch.empty(B, H, Lq, D, device=dev, dtype=q.dtype)
+    lse = torch.empty(B, H, Lq, device=dev, dtype=torch.float32) if need_lse else None
+    a = AttnArgs()
+    a.q = q.data_ptr()
+    a.q_stride = _s3(q)
+    if use_main:
+        a.k, a.v = k.data_ptr(), v.data_ptr()
+        a.k_stride, a.v_stride = _s3(k), _s3(v)
+    a.q_rows, a.kv_rows = _ptr(q_rows), _ptr(kv_rows)
+    a.use_main = 1 if use_main else 0
+    if block_mask is not None:
+        if block_mask.dtype == torch.bool:
+            block_mask = block_mask.view(torch.uint8)
+        nbq, nbk = (Lq + BLOCK - 1) // BLOCK, (Lk + BLOCK - 1) // BLOCK
+        if block_mask.shape[2] < nbq or block_mask.shape[3] < nbk:
+            raise ValueError(f"block_mask {tuple(block_mask.shape)} too small for {nbq}x{nbk} blocks")
+        if block_mask.stride(3) != 1:
+            block_mask = block_mask.contiguous()
+        a.block_mask = block_mask.data_ptr()
+        a.mask_stride = (ctypes.c_int64 * 3)(block_mask.stride(0), block_mask.stride(1),
+                                             block_mask.stride(2))
+    if kp is not None:
+        a.kp, a.vp = kp.data_ptr(), vp.data_ptr()
+        a.kp_stride, a.vp_stride = _s3(kp), _s3(vp)
+        a.Lkp = kp.shape[2]
+        a.kp_log_bias = float(kp_log_bias)
+    a.out = out.data_ptr()
+    a.out_stride = _s3(out)
+    a.lse = _ptr(lse)
+    a.B, a.H, a.Lq, a.Lk, a.D = B, H, Lq, Lk, D
+    a.scale = float(scale) if scale else 0.0
+    a.dtype = _dtype_code(q)
+    check(_lib.load().vb_attn_fwd(ctypes.byref(a), _stream(dev)), "vb_attn_fwd")
+    return (out, lse) if need_lse else out
+
+
+def block_sparse_attn_fwd(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k, head_mask_type,
+                          streaming_info, base_blockmask, max_seqlen_q, max_seqlen_k,
+                          p_dropout=0.0, deterministic=False, softmax_scale=None,
+                          is_causal=False, exact_streaming=False):
+    """Forward of block_sparse_attn_func through vb_block_sparse_attn_fwd (varlen layout).
+    Returns (out_unpad [total_q,H,D], softmax_lse fp32 [B,H,max_seqlen_q])."""
+    dev = _require_gpu(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k, base_blockmask)
+    q_unpad, k_unpad, v_unpad = q_unpad.contiguous(), k_unpad.contiguous(), v_unpad.contiguous()
+    B = cu_seqlens_q.numel() - 1
+    H, D = q_unpad.shape[1], q_unpad.shape[2]
+    nbq = (max_seqlen_q + BLOCK - 1) // BLOCK
+    nbk = (max_seqlen_k + BLOCK - 1) // BLOCK
+    mask = None
+    if base_blockmask is not None:
+        mask = base_blockmask[:, :, :nbq, :nbk]
+        if mask.dtype == torch.bool:
+            mask = mask.contiguous().view(torch.uint8)
+        mask = mask.to(torch.uint8).contiguous()
+    hmt = head_mask_type.to(device=dev, dtype=torch.int32).contiguous() if head_mask_type is not None else None
+    out = torch.empty_like(q_unpad)
+    lse = torch.empty(B, H, max_seqlen_q, device=dev, dtype=torch.float32)
+    check(_lib.load().vb_block_sparse_attn_fwd(
+        q_unpad.data_ptr(), k_unpad.data_ptr(), v_unpad.data_ptr(),
+        cu_seqlens_q.to(torch.int32).contiguous().data_ptr(),
+        cu_seqlens_k.to(torch.int32).contiguous().data_ptr(),
+        _ptr(hmt), _ptr(streaming_info), _ptr(mask), B, H, D, int(max_seqlen_q),
+        int(max_seqlen_k), float(p_dropout), int(bool(deterministic)),
+        float(softmax_scale) if softmax_scale else 0.0, int(bool(is_causal)),
+        int(bool(exact_streaming)), _dtype_code(q_unpad), out.data_ptr(), lse.data_ptr(),
+        _stream(dev)), "vb_block_sparse_attn_fwd")
+    return out, lse
+
+
+# ----------------------------------------------------------------------------------------------
+# mask predictor, energy rule, pooling, combine
+# ----------------------------------------------------------------------------------------------
+def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_keep=1,
+                 max_keep=1, force_tail=0, scale=None, mask_count=None):
+    """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
+    po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb]."""
+    dev = _require_gpu(q, k, q_off, k_off, rows)
+    q, k = _aligned_bhld(q), _aligned_bhld(k)
+    B, H, L, D = q.shape
+    nb = (L + BLOCK - 1) // BLOCK
+    po = torch.empty(B, H, nb, nb, device=dev, dtype=q.dtype)
+    mask = torch.empty(B, H, nb, nb, device=dev, dtype=torch.uint8)
+    q_off = q_off.to(torch.int32).contiguous()
+    k_off = k_off.to(torch.int32).contiguous()
+    a = PredictArgs()
+    a.q, a.k = q.data_ptr(), k.data_ptr()
+    a.q_stride, a.k_stride = _s3(q), _s3(k)
+    a.rows, a.q_off, a.k_off = _ptr(rows), q_off.data_ptr(), k_off.data_ptr()
+    a.B, a.H, a.L, a.D, a.block, a.num_keep = B, H, L, D, BLOCK, q_off.shape[-1]
+    a.scale = float(scale) if scale else 0.0
+    a.energy_threshold = float(energy_threshold)
+    a.min_keep, a.max_keep, a.force_tail = int(min_keep), int(max_keep), int(force_tail)
+    a.po, a.mask, a.mask_count = po.data_ptr(), mask.data_ptr(), _ptr(mask_count)
+    a.dtype = _dtype_code(q)
+    check(_lib.load().vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
+    return po, mask
+
+
+def energy_mask(po, *, energy_threshold=0.95, min_keep=1, max_keep=1, force_tail=0, mask_count=None):
+    """vb_energy_mask on scores po [B,H,nr,nc] (bf16/fp16) -> uint8 mask."""
+    dev = _require_gpu(po)
+    po = po.contiguous()
+    B, H, nr, nc = po.shape
+    mask = torch.empty(B, H, nr, nc, device=dev, dtype=torch.uint8)
+    check(_lib.load().vb_energy_mask(po.data_ptr(), B, H, nr, nc, float(energy_threshold),
+                                     int(min_keep), int(max_keep), int(force_tail),
+                                     _dtype_code(po), mask.data_ptr(), _ptr(mask_count),
+                                     _stream(dev)), "vb_energy_mask")
+    return mask
+
+
+def pool_kv(k, v, gap: int, rows=None):
+    """vb_pool_kv: mean over `gap` consecutive reordered tokens (replicate pad) -> kp, vp."""
+    dev = _require_gpu(k, v, rows)
+    k, v = _aligned_bhld(k), _aligned_bhld(v)
+    B, H, L, D = k.shape
+    Lp = (L + gap - 1) // gap
+    kp = torch.empty(B, H, Lp, D, device=dev, dtype=k.dtype)
+    vp = torch.empty(B, H, Lp, D, device=dev, dtype=v.dtype)
+    check(_lib.load().vb_pool_kv(k.data_ptr(), v.data_ptr(), ctypes.cast(_s3(k), ctypes.c_void_p),
+                                 ctypes.cast(_s3(v), ctypes.c_void_p), _ptr(rows), B, H, L, D,
+                                 int(gap), _dtype_code(k), kp.data_ptr(), vp.data_ptr(),
+                                 _stream(dev)), "vb_pool_kv")
+    return kp, vp
+
+
+def lse_combine(out1, lse1, out2, lse2, gap: float):
+    """vb_lse_combine (reference-faithful eager rounding). Returns (out, alpha fp32 [B,H,L])."""
+    dev = _require_gpu(out1, lse1, out2, lse2)
+    out1, out2 = out1.contiguous(), out2.contiguous()
+    lse1, lse2 = lse1.float().contiguous(), lse2.float().contiguous()
+    B, H, L, D = out1.shape
+    out = torch.empty_like(out1)
+    alpha = torch.empty(B, H, L, device=dev, dtype=torch.float32)
+    check(_lib.load().vb_lse_combine(out1.data_ptr(), lse1.data_ptr(), out2.data_ptr(),
+                                     lse2.data_ptr(), B, H, L, D, float(gap), _dtype_code(out1),
+                                     out.data_ptr(), alpha.data_ptr(), _stream(dev)),
+          "vb_lse_combine")
+    return out, alpha
+
+
+def default_scale(D: int) -> float:
+    return 1.0 / math.sqrt(D)
