@@ -1,0 +1,12 @@
+#!/bin/bash
+# first GPU validation: gpu tests (no -x, to see every failure), then a short bench
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+tail -40 gpurun_out/pytest_gpu.log
+if [ $rc -eq 0 ] || [ $rc -eq 1 ]; then
+  timeout -k 10 400 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1
+  echo "bench rc=$?"
+  tail -5 gpurun_out/bench.log
+fi

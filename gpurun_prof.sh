@@ -1,0 +1,8 @@
+#!/bin/bash
+mkdir -p gpurun_out/prof
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
+echo "rc=$?"
+ls -R gpurun_out/prof | head -20
+f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
+cat "$f" | head -20
