@@ -189,8 +189,8 @@ def measure_kernels(mod, sets, L, H, D, dev, ops, args):
     recs = []
     for s, (q, k, v) in enumerate(sets):
         _, mask = mod.predict_mask(q, k)
-        kp, vp = ops.pool_kv(k, v, mod.sample_gap, rows)
-        recs.append((q, k, v, mask, kp, vp))
+        kp, vp, k_r, v_r = ops.pool_kv(k, v, mod.sample_gap, rows, reordered=True)
+        recs.append((q, k_r, v_r, mask, kp, vp))
     n_rep = 10
     flops = 0.0
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -198,14 +198,14 @@ def measure_kernels(mod, sets, L, H, D, dev, ops, args):
     i = 0
     for _ in range(2):   # warm
         for q, k, v, mask, kp, vp in recs:
-            ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kv_rows=rows, kp=kp, vp=vp,
-                              kp_log_bias=math.log(mod.sample_gap))
+            ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
+                              kp_log_bias=math.log(mod.sample_gap), heavy_rows=mod.force_tail)
     for _ in range(n_rep):
         for q, k, v, mask, kp, vp in recs:
             a, b = ev[i]
             a.record(stream)
-            ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kv_rows=rows, kp=kp, vp=vp,
-                              kp_log_bias=math.log(mod.sample_gap))
+            ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
+                              kp_log_bias=math.log(mod.sample_gap), heavy_rows=mod.force_tail)
             b.record(stream)
             flops += attn_flops(mask, L, D, kp.shape[2])
             i += 1

@@ -96,6 +96,8 @@ typedef struct vb_attn_args {
   int B, H, Lq, Lk, D;
   float scale;            /* <= 0 -> D^-1/2 */
   int dtype;
+  int heavy_rows;         /* scheduling hint: the last N q-block rows keep (almost) every key
+                             block (CogVideoX's forced text rows: 2); 0 = none. Never affects results. */
 } vb_attn_args;
 int vb_attn_fwd(const vb_attn_args* args, void* stream);
 
@@ -136,10 +138,12 @@ int vb_energy_mask(const void* po, int B, int H, int nr, int nc, float energy_th
 /* ------------------------------------------------------------------------------------------
  * Mean pooling of K and V over `gap` consecutive reordered tokens with replicate padding
  * (simple_pooling, cogvideo_blocksparseattn.py:83-88): kp/vp [B,H,ceil(L/gap),D] contiguous.
+ * Optionally (k_r, v_r non-NULL) also writes the reordered copies k_r/v_r [B,H,L,D] contiguous
+ * (the reference's index_select, :148-150) in the same pass: every row is read once.
  * ------------------------------------------------------------------------------------------ */
 int vb_pool_kv(const void* k, const void* v, const int64_t* k_stride, const int64_t* v_stride,
                const int32_t* rows, int B, int H, int L, int D, int gap, int dtype, void* kp,
-               void* vp, void* stream);
+               void* vp, void* k_r, void* v_r, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Reference-faithful LSE combine (cogvideo_blocksparseattn.py:374-393, each eager op rounded to

@@ -90,7 +90,7 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     p = _lib.PredictArgs()
     assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
     assert lib.vb_energy_mask(None, 1, 1, 1, 1, 0.95, 1, 1, 0, 0, None, None, None) == _lib.VB_ERR_INVALID
-    assert lib.vb_pool_kv(None, None, None, None, None, 1, 1, 1, 64, 15, 0, None, None, None) == _lib.VB_ERR_INVALID
+    assert lib.vb_pool_kv(None, None, None, None, None, 1, 1, 1, 64, 15, 0, None, None, None, None, None) == _lib.VB_ERR_INVALID
     assert lib.vb_lse_combine(None, None, None, None, 1, 1, 1, 64, 15.0, 0, None, None, None) == _lib.VB_ERR_INVALID
 
 

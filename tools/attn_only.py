@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Run only the fused attention kernel (and optionally the predictor) N times on CogVideoX / Wan
+shapes — a target for rocprofv3 counter collection."""
+import math
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
+sys.path.insert(0, ROOT)
+import vblade  # noqa: E402
+from vblade import ops  # noqa: E402
+from bench import realistic_qkv  # noqa: E402
+
+variant = sys.argv[1] if len(sys.argv) > 1 else "cog"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+what = sys.argv[3] if len(sys.argv) > 3 else "attn"
+H, D = (48, 64) if variant == "cog" else (12, 128)
+m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+L = m.gilbert_rearranger.seq_len
+dev = torch.device("cuda")
+with torch.no_grad():
+    q, k, v = realistic_qkv(H, L, D, 0, dev)
+    rows = m._rows(dev)
+    qo = vblade.draw_sample_offsets(1, H, dev)
+    ko = vblade.draw_sample_offsets(1, H, dev)
+    _, mask = m.predict_mask(q, k, qo, ko)
+    kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
+    for _ in range(n):
+        if what in ("attn", "all"):
+            ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
+                              kp_log_bias=math.log(m.sample_gap))
+        if what in ("pred", "all"):
+            m.predict_mask(q, k, qo, ko)
+    torch.cuda.synchronize()
+print("done")

@@ -19,6 +19,8 @@
 //                                        the S^T accumulator registers (no LDS round trip)
 // Gilbert reorder: q/k/v rows are gathered through q_rows / kv_rows and O/LSE scattered through
 // q_rows, so the reference's index_select + cat + reverse (:141-161) cost no pass of their own.
+#include <cstdlib>
+
 #include "vb_common.hpp"
 
 namespace vb {
@@ -37,7 +39,16 @@ struct FwdParams {
   float* lse; int64_t lse_s[2];               // row stride 1
   int B, H, Lq, Lk, nbq, nbk;
   float c;                                    // softmax scale * log2(e)
+  int heavy_rows;                             // last q-block rows known to be dense (scheduling hint)
+  int dbg;                                    // diagnostic builds only (VB_DEBUG_ATTN)
 };
+
+#ifndef VB_DIAG
+#define VB_DIAG 0
+#endif
+#ifndef VB_FWD_WAVES_D64
+#define VB_FWD_WAVES_D64 3  // waves per SIMD the D=64 kernel is register-budgeted for
+#endif
 
 constexpr int kThreads = 256;
 constexpr int kQBlk = 128;   // rows per workgroup (4 waves x 32)
@@ -69,8 +80,16 @@ __device__ __forceinline__ typename T::vec8 lds_b128(const uint8_t* base, int of
 }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+// ds_read_b64_tr_b16 issued from inline asm: hipcc's waitcnt pass treats the builtin form as
+// possibly aliasing the in-flight LDS-DMA writes and drains the whole DMA ring (vmcnt(0)) before
+// it. The asm form is invisible to that pass, so its result must be waited for explicitly with
+// vwait_tr() (a lgkmcnt(0) that names the destinations) before any use.
 __device__ __forceinline__ s16x4 lds_tr4(const uint8_t* base, int off) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + off));
+  const uint32_t a = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)(base + off)));
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
 }
 
 template <class T>
@@ -90,42 +109,25 @@ __device__ __forceinline__ typename T::vec8 pack8(const f32x16& acc, int base) {
   return __builtin_bit_cast(typename T::vec8, u);
 }
 
-// Global -> register staging of one 64-key tile of K and V (each thread: CH*64/256 chunks).
-template <int D>
-struct Stage {
-  static constexpr int CH = D / 8;                      // 16-byte chunks per row
-  static constexpr int N = kKT * CH / kThreads;         // chunks per thread per matrix (2 or 4)
-  u32x4 kr[N];
-  u32x4 vr[N];
-};
-
-template <int D>
-__device__ __forceinline__ void stage_load(Stage<D>& st, const uint8_t* kbase, const uint8_t* vbase,
-                                           int64_t krow_stride, int64_t vrow_stride,
-                                           const int32_t* rows, int kstart, int klen) {
-  constexpr int CH = Stage<D>::CH;
-#pragma unroll
-  for (int i = 0; i < Stage<D>::N; ++i) {
-    const int c = threadIdx.x + i * kThreads;
-    const int r = c / CH, ch = c % CH;
-    int kr = kstart + min(r, klen - 1);
-    if (rows) kr = rows[kr];
-    st.kr[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)kr * krow_stride + ch * 16);
-    st.vr[i] = *reinterpret_cast<const u32x4*>(vbase + (int64_t)kr * vrow_stride + ch * 16);
-  }
+#if VB_DIAG
+// diagnostic-only cycle stamps (never in the product build): per-segment sums of s_memtime
+__device__ unsigned long long g_vb_stamp[16];
+__device__ __forceinline__ unsigned long long vb_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
 }
+#define VB_STAMP(var) const unsigned long long var = vb_stamp()
+#define VB_ACC(i, d) acc_st[i] += (d)
+#else
+#define VB_STAMP(var)
+#define VB_ACC(i, d)
+#endif
 
-template <int D>
-__device__ __forceinline__ void stage_store(const Stage<D>& st, uint8_t* kl, uint8_t* vl) {
-  constexpr int CH = Stage<D>::CH;
-#pragma unroll
-  for (int i = 0; i < Stage<D>::N; ++i) {
-    const int c = threadIdx.x + i * kThreads;
-    const int r = c / CH, ch = c % CH;
-    *reinterpret_cast<u32x4*>(kl + k_off<D>(r, ch)) = st.kr[i];
-    *reinterpret_cast<u32x4*>(vl + v_off_bytes<D>(r, ch * 8)) = st.vr[i];
-  }
-}
+// s_waitcnt vmcnt(n) with lgkm/exp counters left at max (gfx9 encoding)
+#define VB_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
 
 // Describes where tile t's keys come from.
 struct TileSrc {
@@ -134,25 +136,51 @@ struct TileSrc {
   int klen;     // valid keys in this tile (1..64)
 };
 
-template <int D, class T, bool kPool>
-__global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(const FwdParams p) {
-  constexpr int KS = D / 16;   // k-steps of the QK^T product
-  constexpr int DT = D / 32;   // 32-wide d tiles of the output
-  constexpr int kTileBytes = kKT * D * 2;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * kTileBytes + kMaxBlocks * 2 + 16];
-  // buffer i: K image at smem + 2*i*kTileBytes, V image right after it
-  uint16_t* list = reinterpret_cast<uint16_t*>(smem + 4 * kTileBytes);
-  int* list_n = reinterpret_cast<int*>(smem + 4 * kTileBytes + kMaxBlocks * 2);
+template <int D, class T, bool kPool, bool kKvRows>
+__global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) attn_fwd_kernel(const FwdParams p) {
+  constexpr int KS = D / 16;                   // k-steps of the QK^T product
+  constexpr int DT = D / 32;                   // 32-wide d tiles of the output
+  constexpr int kRowB = D * 2;                 // bytes per key row
+  constexpr int kMatBytes = kKT * kRowB;       // one 64-key K (or V) tile
+  constexpr int kBufBytes = 2 * kMatBytes;     // K image then V image
+  constexpr int kBufs = (D == 64) ? 3 : 2;     // LDS ring: tile t read, t+1 (and t+2) in flight
+  constexpr int kChunks = kRowB / 16;          // 16-byte chunks per row
+  constexpr int kRowsPerInst = 1024 / kRowB;   // rows one 1-KiB LDS-DMA wave-instruction fills
+  constexpr int kInstPerMat = kMatBytes / 1024;
+  constexpr int kInstPerWave = 2 * kInstPerMat / 4;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kBufs * kBufBytes + kMaxBlocks * 2 + 16];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
+  int* list_n = reinterpret_cast<int*>(smem + kBufs * kBufBytes + kMaxBlocks * 2);
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5;
   const int l32 = lane & 31;
 
-  // heavy-first order: the last q-blocks (CogVideoX's dense text rows) of every head first
+  // Work order (placement only affects speed, never results). Workgroups are dealt round-robin
+  // over the 8 XCDs (blockIdx % 8 share one XCD and its 4 MiB L2).
+  //  phase 1: the `heavy_rows` last q-block rows of every head (CogVideoX's dense text rows, the
+  //           longest workgroups) go first, spread over all XCDs;
+  //  phase 2: every XCD takes a contiguous, head-major range of the remaining (head, q-block)
+  //           work, so the pooled K/V and the kept K/V blocks of the one or two heads an XCD is
+  //           working on are re-read from its own L2 instead of the Infinity Cache / HBM.
   const int BH = p.B * p.H;
-  const int qblk = p.nbq - 1 - (int)(blockIdx.x / BH);
-  const int bh = blockIdx.x % BH;
+  const int hr = min(p.heavy_rows, p.nbq);
+  const int n_heavy = hr * BH;
+  int qblk, bh;
+  if ((int)blockIdx.x < n_heavy) {
+    qblk = p.nbq - 1 - (int)(blockIdx.x / BH);
+    bh = blockIdx.x % BH;
+  } else {
+    const int rows_left = p.nbq - hr;
+    const int id = blockIdx.x - n_heavy;
+    const int nwg = rows_left * BH;
+    const int xcd = id & 7, slot = id >> 3;
+    const int q8 = nwg >> 3, r8 = nwg & 7;
+    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+    bh = lin / rows_left;
+    qblk = rows_left - 1 - lin % rows_left;
+  }
   const int b = bh / p.H, h = bh % p.H;
 
   int Lq = p.Lq, Lk = p.Lk;
@@ -210,15 +238,32 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(const FwdParams p
     }
     if (lane == 0) *list_n = n;
   }
-  __syncthreads();
-  const int nkept = *list_n;
+
+  // ---- Q fragment (B operand of S^T = K.Q^T): row l32 of this wave, d = 16s + 8*half + j --------
+  const int qg = q0 + wave * 32 + l32;               // reordered query position
+  const bool qvalid = qg < Lq;
+  int qrow = qvalid ? qg : Lq - 1;
+  if (p.q_rows) qrow = p.q_rows[qrow];
+  const uint8_t* qbase = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + qrow0 * p.qs[2]);
+  typename T::vec8 qf[KS];
+  {
+    const uint8_t* qp = qbase + (int64_t)qrow * 2 * p.qs[2];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
+    // Launder the Q fragment through an empty asm: the loop's MFMAs then depend on the asm, not
+    // on the global loads, so hipcc's waitcnt pass does not count them against the DMA ring.
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]));
+  }
+  __syncthreads();   // kept-block list visible; Q loads retired before the DMA ring starts
+  const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
   // main tiles: two 64-key halves per kept block, minus an empty second half of the last block
   int ntm = 2 * nkept;
   if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kQBlk + kKT >= Lk) ntm -= 1;
   const int ntp = kPool ? (p.Lkp + kKT - 1) / kKT : 0;
   const int ntiles = ntm + ntp;
 
-  const uint8_t* qbase = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + qrow0 * p.qs[2]);
   const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + krow0 * p.ks[2]);
   const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + krow0 * p.vs[2]);
   const uint8_t* kpbase = nullptr;
@@ -228,10 +273,10 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(const FwdParams p
     vpbase = reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1]);
   }
 
-  auto tile_src = [&](int t) -> TileSrc {
+  auto tile_src = [&](int t) __attribute__((always_inline)) -> TileSrc {
     TileSrc s;
     if (t < ntm) {
-      const int blk = list[t >> 1];
+      const int blk = __builtin_amdgcn_readfirstlane(list[t >> 1]);  // provably wave-uniform
       s.pooled = 0;
       s.kstart = blk * kQBlk + (t & 1) * kKT;
       s.klen = min(kKT, Lk - s.kstart);
@@ -242,26 +287,49 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(const FwdParams p
     }
     return s;
   };
-  auto load_tile = [&](Stage<D>& st, int t) {
-    const TileSrc s = tile_src(t);
-    if (!kPool || !s.pooled)
-      stage_load<D>(st, kbase, vbase, 2 * p.ks[2], 2 * p.vs[2], p.kv_rows, s.kstart, s.klen);
-    else
-      stage_load<D>(st, kpbase, vpbase, 2 * p.kps[2], 2 * p.vps[2], nullptr, s.kstart, s.klen);
-  };
 
-  // ---- Q fragment (B operand of S^T = K.Q^T): row l32 of this wave, d = 16s + 8*half + j --------
-  const int qg = q0 + wave * 32 + l32;               // reordered query position
-  const bool qvalid = qg < Lq;
-  int qrow = qvalid ? qg : Lq - 1;
-  if (p.q_rows) qrow = p.q_rows[qrow];
-  typename T::vec8 qf[KS];
-  {
-    const uint8_t* qp = qbase + (int64_t)qrow * 2 * p.qs[2];
+  // Tile t -> LDS ring slot t % kBufs by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+  // wave-instruction, written linearly). The images' XOR swizzles (k_off / v_off_bytes) are
+  // applied to each lane's SOURCE chunk instead: LDS slot `sl` of row r holds the chunk that
+  // k_off / v_off_bytes would have placed there. Waves 0-1 (D=64) fill K, waves 2-3 fill V.
+  // every wave fills ONE matrix: waves 0-1 -> K, waves 2-3 -> V (kInstPerWave*2 == kInstPerMat)
+  static_assert(2 * kInstPerWave == kInstPerMat, "DMA split assumes two waves per matrix");
+  const int my_mat = wave >> 1;
+  const uint8_t* my_base = my_mat == 0 ? kbase : vbase;
+  const int64_t my_stride = 2 * (my_mat == 0 ? p.ks[2] : p.vs[2]);
+  const uint8_t* my_pbase = my_mat == 0 ? kpbase : vpbase;
+  const int64_t my_pstride = kPool ? 2 * (my_mat == 0 ? p.kps[2] : p.vps[2]) : 0;
+  // source chunk of every DMA lane (fixed: the image row of lane L is a function of L only)
+  int my_chunk[kInstPerWave];
+  int my_row[kInstPerWave];
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-      qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
+  for (int i = 0; i < kInstPerWave; ++i) {
+    const int mi = (wave & 1) * kInstPerWave + i;
+    const int r = mi * kRowsPerInst + lane / kChunks;
+    const int sl = lane % kChunks;
+    my_row[i] = r;
+    if (my_mat == 0) {
+      my_chunk[i] = sl ^ ((D == 64) ? ((r >> 1) & 7) : (r & 15));
+    } else {
+      const int vsw = (D == 64) ? ((r >> 1) & 1) : (r & 3);
+      my_chunk[i] = (((sl >> 2) ^ vsw) << 2) | (sl & 3);
+    }
   }
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    const TileSrc src = tile_src(t);
+    uint8_t* dst = smem + (t % kBufs) * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
+    const bool pooled = kPool && src.pooled;
+    const uint8_t* base = pooled ? my_pbase : my_base;
+    const int64_t stride = pooled ? my_pstride : my_stride;
+#pragma unroll
+    for (int i = 0; i < kInstPerWave; ++i) {
+      int key = src.kstart + min(my_row[i], src.klen - 1);
+      if (kKvRows && !pooled) key = p.kv_rows[key];  // gathered k/v rows (slower: serialises the ring)
+      const uint8_t* gsrc = base + (int64_t)key * stride + my_chunk[i] * 16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+    }
+  };
 
   f32x16 o[DT];
 #pragma unroll
@@ -271,85 +339,145 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(const FwdParams p
   float m = -INFINITY;  // running max (exp2 domain) of this lane's query row
   float l = 0.f;        // running partial row sum (this half's keys)
 
-  Stage<D> st;
-  if (ntiles > 0) {
-    load_tile(st, 0);
-    stage_store<D>(st, smem, smem + kTileBytes);
-  }
-  __syncthreads();
+  const int vrow = 4 * half + (lane & 15) / 4;
+  const int vcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+#if VB_DIAG
+  unsigned long long acc_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) load_tile(st, t + 1);
-    const TileSrc src = tile_src(t);
-    const float bias = (kPool && src.pooled) ? p.pool_bias_l2 : 0.f;
-    const uint8_t* kl = smem + cur * 2 * kTileBytes;
-    const uint8_t* vl = kl + kTileBytes;
-
-    // S^T = K . Q^T : two 32-key output tiles
+  // One 64-key tile: S^T = K.Q^T, online softmax, O^T += V^T.P^T.
+  auto tile_step = [&](const uint8_t* kl, const uint8_t* vl, float bias, int klen) __attribute__((always_inline)) {
     f32x16 s[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
+      typename T::vec8 kf[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(kl, k_off<D>(kt * 32 + l32, 2 * ks + half));
 #pragma unroll
       for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const typename T::vec8 a = lds_b128<T>(kl, k_off<D>(kt * 32 + l32, 2 * ks + half));
-        s[kt] = T::mfma32(a, qf[ks], s[kt]);
-      }
+      for (int ks = 0; ks < KS; ++ks) s[kt] = T::mfma32(kf[ks], qf[ks], s[kt]);
     }
-    // scale, bias, tail mask, row max
-    float mt = -INFINITY;
+    // V^T fragments (ds_read_b64_tr_b16) for the first VPRE k-steps, issued before the softmax
+    // VALU so they land while it runs; the rest are fetched one k-step ahead inside the PV loop.
+    constexpr int VPRE = (D == 64) ? 4 : 2;
+    s16x4 vlo[4][DT], vhi[4][DT];
+    auto read_v = [&](int kk) __attribute__((always_inline)) {
+      const int kb = (kk >> 1) * 32 + 16 * (kk & 1) + vrow;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        float x = s[kt][r] * p.c + bias;
-        if (key >= src.klen) x = -INFINITY;
-        s[kt][r] = x;
-        mt = fmaxf(mt, x);
+      for (int dt = 0; dt < DT; ++dt) {
+        vlo[kk][dt] = lds_tr4(vl, v_off_bytes<D>(kb, dt * 32 + vcol));
+        vhi[kk][dt] = lds_tr4(vl, v_off_bytes<D>(kb + 8, dt * 32 + vcol));
       }
-    mt = max_xor32(mt);
-    const float mn = fmaxf(m, mt);
-    const float alpha = exp2_fast(m - mn);
-    m = mn;
+    };
+    auto wait_v = [&](int kk) __attribute__((always_inline)) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[kk][dt]), "+v"(vhi[kk][dt]));
+    };
+#pragma unroll
+    for (int kk = 0; kk < VPRE; ++kk) read_v(kk);
+    VB_STAMP(s1);
+    if (klen < kKT) {   // tail tile only; the volatile asm keeps it a real (wave-uniform) branch
+      asm volatile("");
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= klen) s[kt][r] = -INFINITY;
+    }
+    // row max: four independent chains (short dependency chains, max3-friendly)
+    float mq[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) mq[c] = fmaxf(s[c >> 1][8 * (c & 1)], s[c >> 1][8 * (c & 1) + 1]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 2; r < 8; ++r) mq[c] = fmaxf(mq[c], s[c >> 1][8 * (c & 1) + r]);
+    float mt = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
+    mt = max_xor32(mt) * p.c + bias;            // tile row max, exp2 domain
+    // lazy rescale: only when some row's running max grows (exact; no threshold). The empty
+    // volatile asm keeps hipcc from if-converting this rare block into every iteration.
+    if (!__all(mt <= m)) {
+      asm volatile("");
+      const float mn = fmaxf(m, mt);
+      const float alpha = exp2_fast(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < DT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    }
+    const float nbias = bias - m;
     float ls = 0.f;
+    if (VB_DIAG && (p.dbg & 1)) {   // diagnostic: no exp
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = exp2_fast(s[kt][r] - mn);
-        s[kt][r] = e;
-        ls += e;
-      }
-    l = l * alpha + ls;
+        for (int r = 0; r < 16; ++r) {
+          const float e = fmaf(s[kt][r], p.c, nbias);
+          s[kt][r] = e;
+          ls += e;
+        }
+    } else {
+      float lq[4] = {0.f, 0.f, 0.f, 0.f};   // four independent partial sums
 #pragma unroll
-    for (int i = 0; i < DT; ++i)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-
+        for (int r = 0; r < 16; ++r) {
+          const float e = exp2_fast(fmaf(s[kt][r], p.c, nbias));
+          s[kt][r] = e;
+          lq[(2 * kt + r) & 3] += e;
+        }
+      ls = (lq[0] + lq[1]) + (lq[2] + lq[3]);
+    }
+    l += ls;
+    VB_STAMP(s2);
+    VB_ACC(3, s2 - s1);
     // O^T += V^T . P^T : 4 k-steps of 16 keys
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      const int kt = kk >> 1, sp = kk & 1;
-      const typename T::vec8 pf = pack8<T>(s[kt], 8 * sp);
-      const int kb = kt * 32 + 16 * sp + 4 * half + (lane & 15) / 4;  // this lane's block row
+      wait_v(kk);
+      if (kk + VPRE < 4) read_v(kk + VPRE);
+      const typename T::vec8 pf = pack8<T>(s[kk >> 1], 8 * (kk & 1));
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-        const s16x4 lo = lds_tr4(vl, v_off_bytes<D>(kb, col));
-        const s16x4 hi = lds_tr4(vl, v_off_bytes<D>(kb + 8, col));
-        o[dt] = T::mfma32(join8<T>(lo, hi), pf, o[dt]);
-      }
+      for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo[kk][dt], vhi[kk][dt]), pf, o[dt]);
     }
+    VB_STAMP(s3);
+    VB_ACC(4, s3 - s2);
+  };
 
-    if (t + 1 < ntiles) {
-      uint8_t* kn = smem + (cur ^ 1) * 2 * kTileBytes;
-      stage_store<D>(st, kn, kn + kTileBytes);
-    }
-    __syncthreads();
+  for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
+  for (int t = 0; t < ntiles; ++t) {
+    VB_STAMP(t0);
+    // retire this wave's DMAs of tile t (younger tiles stay in flight); the barrier then makes
+    // every wave's part visible and proves slot (t-1) % kBufs is no longer being read
+    const int younger = min(ntiles - 1 - t, kBufs - 2);
+    if (younger >= 2) VB_WAIT_VMCNT(2 * kInstPerWave);
+    else if (younger == 1) VB_WAIT_VMCNT(kInstPerWave);
+    else VB_WAIT_VMCNT(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    VB_STAMP(t1);
+    VB_ACC(0, t1 - t0);
+    if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
+    VB_STAMP(t2);
+    VB_ACC(1, t2 - t1);
+    const TileSrc src = tile_src(t);
+    const float bias = (kPool && src.pooled) ? p.pool_bias_l2 : 0.f;
+    const uint8_t* kl = smem + (t % kBufs) * kBufBytes;
+    if (VB_DIAG && (p.dbg & 2)) continue;   // diagnostic: stream tiles only
+    tile_step(kl, kl + kMatBytes, bias, src.klen);
+    VB_STAMP(t3);
+    VB_ACC(2, t3 - t2);
   }
+#if VB_DIAG
+  if (lane == 0) {
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_vb_stamp[i], acc_st[i]);
+    atomicAdd(&g_vb_stamp[8], (unsigned long long)ntiles);
+  }
+#endif
 
   // ---- epilogue -----------------------------------------------------------------------------------
   const float lt = add_xor32(l);
@@ -379,10 +507,15 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(const FwdParams p
 template <int D, class T>
 static int launch_fwd(const FwdParams& p, bool pool, hipStream_t stream) {
   const dim3 grid(p.nbq * p.B * p.H);
-  if (pool)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true>), grid, dim3(kThreads), 0, stream, p);
+  const bool rows = p.kv_rows != nullptr;
+  if (pool && rows)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, true>), grid, dim3(kThreads), 0, stream, p);
+  else if (pool)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, false>), grid, dim3(kThreads), 0, stream, p);
+  else if (rows)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, true>), grid, dim3(kThreads), 0, stream, p);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false>), grid, dim3(kThreads), 0, stream, p);
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, false>), grid, dim3(kThreads), 0, stream, p);
   return check_launch("attn_fwd_kernel");
 }
 
@@ -402,6 +535,18 @@ static int dispatch_fwd(const FwdParams& p, int D, int dtype, bool pool, hipStre
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
 }  // namespace vb
+
+#if VB_DIAG
+extern "C" int vb_diag_stamps(unsigned long long* host16, int reset) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(host16, HIP_SYMBOL(vb::g_vb_stamp), sizeof(unsigned long long) * 16);
+  if (reset) {
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(vb::g_vb_stamp), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
 
 extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
   using namespace vb;
@@ -441,6 +586,10 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
   p.B = a->B; p.H = a->H; p.Lq = a->Lq; p.Lk = a->use_main ? a->Lk : 1; p.nbq = nbq; p.nbk = nbk;
   const float scale = a->scale > 0.f ? a->scale : (float)(1.0 / sqrt((double)a->D));
   p.c = scale * kLog2e;
+  p.heavy_rows = a->heavy_rows;
+#if VB_DIAG
+  if (const char* d = getenv("VB_DEBUG_ATTN")) p.dbg = atoi(d);
+#endif
   return dispatch_fwd(p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream));
 }
 

@@ -55,14 +55,14 @@ __device__ __forceinline__ float round_to(float x) {
   return T::to_f32(T::from_f32(x));
 }
 
-// pack two f32 into one dword of two 16-bit elements (lo = a)
+// pack two f32 into one dword of two 16-bit elements (lo = a), round-to-nearest-even;
+// __builtin_convertvector lowers to ONE v_cvt_pk_bf16_f32 (two scalar casts + or would be three)
 template <class T>
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  typename T::raw ra = T::from_f32(a), rb = T::from_f32(b);
-  uint16_t ua, ub;
-  __builtin_memcpy(&ua, &ra, 2);
-  __builtin_memcpy(&ub, &rb, 2);
-  return static_cast<uint32_t>(ua) | (static_cast<uint32_t>(ub) << 16);
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef typename T::raw r2 __attribute__((ext_vector_type(2)));
+  const f32x2 x = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(x, r2));
 }
 
 // ---------------------------------------------------------------- wave helpers

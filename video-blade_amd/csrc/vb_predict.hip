@@ -12,6 +12,8 @@
 //     descending rank, fp32-accumulated cumsum rounded to the storage dtype per prefix, the first
 //     crossing of storage(total * thr), clamp to [min_keep, max_keep], forced tail rows/cols.
 // Nothing but Po and the mask reaches HBM (R stays in LDS).
+#include <cstdlib>
+
 #include "vb_common.hpp"
 
 namespace vb {
@@ -33,7 +35,12 @@ struct PredParams {
   void* po;
   uint8_t* mask;
   unsigned long long* count;
+  int dbg;   // diagnostic builds only (VB_DEBUG_PRED): 1 = skip epilogue, 2 = skip main loop
 };
+
+#ifndef VB_DIAG
+#define VB_DIAG 0
+#endif
 
 // caller row holding reordered-padded position `pos` of a (b,h) stream
 __device__ __forceinline__ int sampled_row(int blk, int off, int block, int L, const int32_t* rows) {
@@ -42,49 +49,90 @@ __device__ __forceinline__ int sampled_row(int blk, int off, int block, int L, c
   return rows ? rows[pos] : pos;
 }
 
-// Energy rule on one row of nc normalised scores held (storage-rounded, as f32) in LDS `val`.
-// `scratch` has room for nc floats. Executed by one full wave. Returns kept count via mask bytes.
+// storage bits of a value already rounded to T (non-negative): orders like the value
 template <class T>
-__device__ int energy_row(const float* val, float* sorted, uint8_t* mrow, int nc, float thr,
+__device__ __forceinline__ uint32_t storage_bits(float v) {
+  const typename T::raw r = T::from_f32(v);
+  uint16_t u;
+  __builtin_memcpy(&u, &r, 2);
+  return u;
+}
+
+// Energy rule on one row of nc normalised scores held (storage-rounded, as f32) in LDS `val`
+// (room for kMaxNb + 4 floats); `keys` is LDS scratch for kMaxNb + 4 uint32. One full wave.
+// Sort key = (storage bits << 16) | (0xFFFF - index): larger value first, ties -> lower index
+// first (a stable descending sort), one unsigned compare per pair. The fp32-accumulated
+// cumulative sum over the sorted values runs sequentially (bit-identical to torch's CPU cumsum)
+// through v_readlane on a register-distributed copy, recording each prefix in its own lane.
+template <class T>
+__device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
                           int min_keep, int max_keep, int force_cols, bool force_all) {
+  constexpr int U = kMaxNb / 64 + 1;
   const int lane = threadIdx.x & 63;
-  // stable descending rank: larger first, equal values lower index first
-  int rank[kMaxNb / 64 + 1];
+  uint32_t mykey[U];
+  int rank[U];
 #pragma unroll
-  for (int u = 0; u < kMaxNb / 64 + 1; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int j = lane + 64 * u;
+    mykey[u] = (j < nc) ? ((storage_bits<T>(val[j]) << 16) | (0xFFFFu - j)) : 0u;
+    if (j < nc) keys[j] = mykey[u];
     rank[u] = 0;
-    if (j < nc) {
-      const float v = val[j];
-      int rk = 0;
-      for (int t = 0; t < nc; ++t) {
-        const float w = val[t];
-        rk += (w > v) || (w == v && t < j);
-      }
-      rank[u] = rk;
-      sorted[rk] = v;
-    }
+  }
+  if (lane < 4) keys[nc + lane] = 0u;  // pad: never greater than a real key
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  for (int t4 = 0; t4 < nc; t4 += 4) {
+    const u32x4 kk = *reinterpret_cast<const u32x4*>(keys + t4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int u = 0; u < U; ++u) rank[u] += (kk[e] > mykey[u]) ? 1 : 0;
+  }
+  // scatter values into sorted order (reuse `keys` as float storage after a wave barrier)
+  __builtin_amdgcn_wave_barrier();
+  float* sorted = reinterpret_cast<float*>(keys);
+  float vals[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = lane + 64 * u;
+    vals[u] = (j < nc) ? val[j] : 0.f;
   }
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
-  int k = 0;
-  if (lane == 0) {
-    float acc = 0.f;
-    for (int t = 0; t < nc; ++t) acc += sorted[t];
-    const float total = round_to<T>(acc);
-    const float th = round_to<T>(total * thr);
-    acc = 0.f;
-    k = nc;
-    for (int t = 0; t < nc; ++t) {
-      acc += sorted[t];
-      if (round_to<T>(acc) >= th) { k = t; break; }
-    }
-    k = min(max(k, min_keep), max_keep);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (lane + 64 * u < nc) sorted[rank[u]] = vals[u];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  float sv[U], pre[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = lane + 64 * u;
+    sv[u] = (t < nc) ? sorted[t] : 0.f;
+    pre[u] = 0.f;
   }
-  k = __shfl(k, 0);
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (64 * u >= nc) break;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      acc += __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(sv[u]), i));  // sv == 0 past nc
+      pre[u] = (lane == i) ? acc : pre[u];
+    }
+  }
+  const float total = round_to<T>(acc);     // cum_energy[..., -1]
+  const float th = round_to<T>(total * thr);
+  int k = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = lane + 64 * u;
+    k += __popcll(__ballot(t < nc && round_to<T>(pre[u]) < th));
+  }
+  k = min(max(k, min_keep), max_keep);
   int kept = 0;
 #pragma unroll
-  for (int u = 0; u < kMaxNb / 64 + 1; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int j = lane + 64 * u;
     if (j < nc) {
       const bool keep = force_all || rank[u] < k || j >= nc - force_cols;
@@ -92,40 +140,59 @@ __device__ int energy_row(const float* val, float* sorted, uint8_t* mrow, int nc
       kept += keep;
     }
   }
-  // wave sum of kept
   for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
   return kept;
 }
 
+// s_waitcnt vmcnt(n) with lgkm/exp counters left at max (gfx9 encoding)
+#define VB_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
+
 template <int D, class T>
-__global__ void __launch_bounds__(kPThreads, 1) mask_predict_kernel(const PredParams p) {
+__global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredParams p) {
   constexpr int KS = D / 16;
-  constexpr int CH = D / 8;
-  constexpr int kTileBytes = kKeysPerTile * D * 2;
-  constexpr int kN = kKeysPerTile * CH / kPThreads;  // staged chunks per thread
-  // LDS: R [4 waves][32 rows][nb] storage dtype | m [4][32] f32 | K tile x2 | row scratch
+  constexpr int kRowB = D * 2;                        // bytes per key row
+  constexpr int kTileBytes = kKeysPerTile * kRowB;
+  constexpr int kRowsPerInst = 1024 / kRowB;          // rows one 1-KiB LDS-DMA wave-instruction fills
+  constexpr int kInstPerWave = kTileBytes / 1024 / kPWaves;
+  constexpr int kBufs = 4;                            // tiles t (read), t+1, t+2 in flight, t+3 issued
+  // LDS: R [4 waves][32 rows][rstride] storage dtype | m [4][32] f32 | sampled-key row table
+  //      [nb][32] u16 | K tiles x4 (after the main loop: per-wave row scratch)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nb = p.nb;
   const int rstride = (nb + 7) & ~7;
   typename T::raw* R = reinterpret_cast<typename T::raw*>(smem);
   const int r_bytes = (kPWaves * 32 * rstride * 2 + 15) & ~15;
   float* mrow_s = reinterpret_cast<float*>(smem + r_bytes);
-  uint8_t* ktile = smem + r_bytes + kPWaves * 32 * 4;
-  float* rowbuf = reinterpret_cast<float*>(ktile + 2 * kTileBytes);  // [4][2][kMaxNb]
+  uint16_t* krow = reinterpret_cast<uint16_t*>(smem + r_bytes + kPWaves * 32 * 4);
+  uint8_t* ktile = smem + r_bytes + kPWaves * 32 * 4 + ((nb * 32 * 2 + 15) & ~15);
+  float* rowbuf = reinterpret_cast<float*>(ktile);  // [4][2][kMaxNb + 4], reused after the loop
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int half = lane >> 5;
   const int l32 = lane & 31;
-  const int bh = blockIdx.y;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 share one),
+  // so give each XCD a contiguous range of (head, q-group) work — a head's sampled keys are then
+  // re-read from that XCD's own L2 instead of the Infinity Cache. Placement only affects speed.
+  const int nqg = (nb + kPWaves - 1) / kPWaves;
+  const int nwg = nqg * p.B * p.H;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int bh = lin / nqg;
   const int b = bh / p.H, h = bh % p.H;
-  const int qb = blockIdx.x * kPWaves + wave;  // this wave's sampled q-block
+  const int qb = (lin % nqg) * kPWaves + wave;  // this wave's sampled q-block
   const bool wave_active = qb < nb;
 
   const uint8_t* qbase = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1]);
   const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1]);
+  const int64_t kstride_b = 2 * p.ks[2];
   const int32_t* qoff = p.q_off + (int64_t)bh * 32;
   const int32_t* koff = p.k_off + (int64_t)bh * 32;
+
+  // caller rows of every sampled key (block j, slot t): one parallel gather, then LDS lookups
+  for (int e = threadIdx.x; e < nb * 32; e += kPThreads)
+    krow[e] = (uint16_t)sampled_row(e >> 5, koff[e & 31], p.block, p.L, p.rows);
 
   // Q fragment of this lane's sampled row (B operand of S^T = K_s . Q_s^T)
   typename T::vec8 qf[KS];
@@ -135,78 +202,82 @@ __global__ void __launch_bounds__(kPThreads, 1) mask_predict_kernel(const PredPa
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]));  // see vb_attn_fwd.hip
   }
   float m = -INFINITY;
+  __syncthreads();   // krow visible; all plain global loads retired before the DMA pipeline
 
-  const int ntiles = (nb + 1) / 2;
-  u32x4 stg[kN];
-  auto load = [&](int t) {
+  const int ntiles = (VB_DIAG && (p.dbg & 2)) ? 0 : (nb + 1) / 2;
+  // K tile t by LDS-DMA (global_load_lds_dwordx4): the LDS image is written linearly (1 KiB per
+  // wave-instruction), so the 16-byte-chunk XOR swizzle of the image is applied to each lane's
+  // SOURCE address: LDS slot `sl` of row r holds chunk sl ^ sw(r).
+  auto issue = [&](int t) {
+    uint8_t* dst = ktile + (t % kBufs) * kTileBytes;
 #pragma unroll
-    for (int i = 0; i < kN; ++i) {
-      const int c = threadIdx.x + i * kPThreads;
-      const int r = c / CH, ch = c % CH;            // r: key within tile (0..63)
-      const int blk = min(2 * t + (r >> 5), nb - 1);
-      const int row = sampled_row(blk, koff[r & 31], p.block, p.L, p.rows);
-      stg[i] = *reinterpret_cast<const u32x4*>(kbase + (int64_t)row * 2 * p.ks[2] + ch * 16);
-    }
-  };
-  auto store = [&](uint8_t* dst) {
-#pragma unroll
-    for (int i = 0; i < kN; ++i) {
-      const int c = threadIdx.x + i * kPThreads;
-      const int r = c / CH, ch = c % CH;
+    for (int i = 0; i < kInstPerWave; ++i) {
+      const int inst = wave * kInstPerWave + i;
+      const int r = inst * kRowsPerInst + lane / (kRowB / 16);       // key row within the tile
+      const int sl = lane % (kRowB / 16);
       const int sw = (D == 64) ? ((r >> 1) & 7) : (r & 15);
-      *reinterpret_cast<u32x4*>(dst + r * D * 2 + 16 * (ch ^ sw)) = stg[i];
+      const int blk = min(2 * t + (r >> 5), nb - 1);
+      const uint8_t* src = kbase + (int64_t)krow[blk * 32 + (r & 31)] * kstride_b + 16 * (sl ^ sw);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + inst * 1024), 16, 0, 0);
     }
   };
-
-  load(0);
-  store(ktile);
-  __syncthreads();
+  for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) load(t + 1);
-    const uint8_t* kl = ktile + cur * kTileBytes;
+    // retire this wave's DMA of tile t (younger tiles stay in flight), then the barrier makes
+    // every wave's part visible and guarantees tile t-1's buffer is no longer being read
+    const int younger = min(ntiles - 1 - t, kBufs - 2);
+    if (younger >= 2) VB_WAIT_VMCNT(2 * kInstPerWave);
+    else if (younger == 1) VB_WAIT_VMCNT(kInstPerWave);
+    else VB_WAIT_VMCNT(0);
+    __builtin_amdgcn_s_barrier();
+    if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
+    const uint8_t* kl = ktile + (t % kBufs) * kTileBytes;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const int j = 2 * t + kt;
-      f32x16 s;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+      typename T::vec8 kf[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const int row = kt * 32 + l32;
         const int sw = (D == 64) ? ((row >> 1) & 7) : (row & 15);
-        const typename T::vec8 a =
-            *reinterpret_cast<const typename T::vec8*>(kl + row * D * 2 + 16 * ((2 * ks + half) ^ sw));
-        s = T::mfma32(a, qf[ks], s);
+        kf[ks] = *reinterpret_cast<const typename T::vec8*>(kl + row * kRowB + 16 * ((2 * ks + half) ^ sw));
       }
-      float mx = -INFINITY;
+      f32x16 s;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s = T::mfma32(kf[ks], qf[ks], s);
+      float mx = fmaxf(s[0], s[1]);
+#pragma unroll
+      for (int r = 2; r < 16; ++r) mx = fmaxf(mx, s[r]);
       mx = max_xor32(mx) * p.c;                       // tl.max(qk, 1) * qk_scale
       if (j < nb) {
         m = fmaxf(m, mx);
         if (half == kt) R[(wave * 32 + l32) * rstride + j] = T::from_f32(mx);
       }
     }
-    if (t + 1 < ntiles) store(ktile + (cur ^ 1) * kTileBytes);
-    __syncthreads();
   }
   if (half == 0) mrow_s[wave * 32 + l32] = m;
   __syncthreads();
-  if (!wave_active) return;
+  if (!wave_active || (VB_DIAG && (p.dbg & 1))) return;
 
-  // Po[qb, j] = storage(max_r exp2(R[r][j] - m_r)); then storage-dtype row normalisation
-  float* val = rowbuf + wave * 2 * kMaxNb;
-  float* sorted = val + kMaxNb;
+  // Po[qb, j] = storage(max_r exp2(R[r][j] - m_r)) = storage(exp2(max_r (R[r][j] - m_r)))
+  // (exp2 and the rounding are monotone), then the storage-dtype row normalisation
+  float* val = rowbuf + wave * 2 * (kMaxNb + 4);
+  uint32_t* keys = reinterpret_cast<uint32_t*>(val + kMaxNb + 4);
   const float* mw = mrow_s + wave * 32;
   const typename T::raw* Rw = R + wave * 32 * rstride;
   float part = 0.f;
   for (int j = lane; j < nb; j += 64) {
-    float cm = 0.f;
-    for (int r = 0; r < 32; ++r) cm = fmaxf(cm, exp2_fast(T::to_f32(Rw[r * rstride + j]) - mw[r]));
-    cm = round_to<T>(cm);
+    float cm = -INFINITY;
+#pragma unroll 8
+    for (int r = 0; r < 32; ++r) cm = fmaxf(cm, T::to_f32(Rw[r * rstride + j]) - mw[r]);
+    cm = round_to<T>(exp2_fast(cm));
     val[j] = cm;
     part += cm;
   }
@@ -222,7 +293,7 @@ __global__ void __launch_bounds__(kPThreads, 1) mask_predict_kernel(const PredPa
   __builtin_amdgcn_wave_barrier();
   uint8_t* mrow = p.mask + ((int64_t)bh * nb + qb) * nb;
   const bool force_all = p.force_tail > 0 && qb >= nb - p.force_tail;
-  const int kept = energy_row<T>(val, sorted, mrow, nb, p.thr, p.min_keep, p.max_keep, p.force_tail, force_all);
+  const int kept = energy_row<T>(val, keys, mrow, nb, p.thr, p.min_keep, p.max_keep, p.force_tail, force_all);
   if (p.count && lane == 0) atomicAdd(p.count, (unsigned long long)kept);
 }
 
@@ -230,7 +301,7 @@ template <class T>
 __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int rows_total, int nc, float thr,
                                                           int min_keep, int max_keep, int force_tail, int nr,
                                                           uint8_t* mask, unsigned long long* count) {
-  __shared__ float buf[4][2 * kMaxNb];
+  __shared__ __attribute__((aligned(16))) float buf[4][2 * (kMaxNb + 4)];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows_total) return;
@@ -241,17 +312,20 @@ __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int ro
   __builtin_amdgcn_wave_barrier();
   const int i = row % nr;
   const bool force_all = force_tail > 0 && i >= nr - force_tail;
-  const int kept = energy_row<T>(val, val + kMaxNb, mask + (int64_t)row * nc, nc, thr, min_keep, max_keep,
-                                 force_tail, force_all);
+  const int kept = energy_row<T>(val, reinterpret_cast<uint32_t*>(val + kMaxNb + 4), mask + (int64_t)row * nc, nc,
+                                 thr, min_keep, max_keep, force_tail, force_all);
   if (count && lane == 0) atomicAdd(count, (unsigned long long)kept);
 }
 
-// simple_pooling of K and V: one thread per 16-byte chunk of a pooled row
+// simple_pooling of K and V: one thread per 16-byte chunk of a pooled row. Every reordered row
+// is read by exactly one thread, which (when k_r/v_r are given) also writes it to the contiguous
+// Gilbert-ordered copies the attention kernel streams (the reference's index_select, fused).
 template <class T>
 __global__ void __launch_bounds__(256) pool_kv_kernel(const uint8_t* k, const uint8_t* v, int64_t ks0, int64_t ks1,
                                                       int64_t ks2, int64_t vs0, int64_t vs1, int64_t vs2,
                                                       const int32_t* rows, int B, int H, int L, int D, int gap,
-                                                      int Lp, uint8_t* kp, uint8_t* vp) {
+                                                      int Lp, uint8_t* kp, uint8_t* vp, uint8_t* k_r,
+                                                      uint8_t* v_r) {
   const int CH = D / 8;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)B * H * Lp * CH;
@@ -265,10 +339,16 @@ __global__ void __launch_bounds__(256) pool_kv_kernel(const uint8_t* k, const ui
 #pragma unroll
   for (int e = 0; e < 8; ++e) ak[e] = av[e] = 0.f;
   for (int t = 0; t < gap; ++t) {
-    int pos = min(pr * gap + t, L - 1);  // replicate padding
+    const int g = pr * gap + t;
+    int pos = min(g, L - 1);  // replicate padding
     if (rows) pos = rows[pos];
     const u32x4 xk = *reinterpret_cast<const u32x4*>(k + 2 * (b * ks0 + h * ks1 + (int64_t)pos * ks2) + ch * 16);
     const u32x4 xv = *reinterpret_cast<const u32x4*>(v + 2 * (b * vs0 + h * vs1 + (int64_t)pos * vs2) + ch * 16);
+    if (k_r && g < L) {
+      const int64_t o = ((int64_t)bh * L + g) * D * 2 + ch * 16;
+      *reinterpret_cast<u32x4*>(k_r + o) = xk;
+      *reinterpret_cast<u32x4*>(v_r + o) = xv;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       ak[2 * e] += T::bits_to_f32(xk[e] & 0xffff);
@@ -328,7 +408,9 @@ __global__ void __launch_bounds__(256) lse_combine_kernel(const uint8_t* out1, c
 static size_t predict_smem_bytes(int nb, int D) {
   const int rstride = (nb + 7) & ~7;
   const size_t r_bytes = ((size_t)kPWaves * 32 * rstride * 2 + 15) & ~size_t(15);
-  return r_bytes + kPWaves * 32 * 4 + 2 * (size_t)kKeysPerTile * D * 2 + (size_t)kPWaves * 2 * kMaxNb * 4;
+  const size_t tiles = 4 * (size_t)kKeysPerTile * D * 2;
+  const size_t scratch = (size_t)kPWaves * 2 * (kMaxNb + 4) * 4;
+  return r_bytes + kPWaves * 32 * 4 + (((size_t)nb * 32 * 2 + 15) & ~size_t(15)) + (tiles > scratch ? tiles : scratch);
 }
 
 template <int D, class T>
@@ -338,7 +420,7 @@ static int launch_predict(const PredParams& p, hipStream_t stream) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)smem) != hipSuccess)
     return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
-  const dim3 grid((p.nb + kPWaves - 1) / kPWaves, p.B * p.H);
+  const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
   return check_launch("mask_predict_kernel");
 }
@@ -354,6 +436,7 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
     return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: block must be 128 and num_keep 32 (the reference's values)");
   const int nb = (a->L + a->block - 1) / a->block;
   if (nb > kMaxNb) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: sequence too long");
+  if (a->L > 65535) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: L must be < 65536");
   if (a->min_keep < 1 || a->max_keep < 1) return fail(VB_ERR_INVALID, "vb_mask_predict: keep counts must be >= 1");
   for (int i = 0; i < 3; ++i)
     if ((a->q_stride[i] | a->k_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_mask_predict: strides must be multiples of 8");
@@ -367,6 +450,9 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   p.thr = a->energy_threshold;
   p.min_keep = a->min_keep; p.max_keep = a->max_keep; p.force_tail = a->force_tail;
   p.po = a->po; p.mask = a->mask; p.count = a->mask_count;
+#if VB_DIAG
+  if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);
+#endif
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a->dtype == VB_DTYPE_BF16) {
     if (a->D == 64) return launch_predict<64, BF16>(p, s);
@@ -404,9 +490,10 @@ extern "C" int vb_energy_mask(const void* po, int B, int H, int nr, int nc, floa
 
 extern "C" int vb_pool_kv(const void* k, const void* v, const int64_t* k_stride, const int64_t* v_stride,
                           const int32_t* rows, int B, int H, int L, int D, int gap, int dtype, void* kp, void* vp,
-                          void* stream) {
+                          void* k_r, void* v_r, void* stream) {
   using namespace vb;
   if (!k || !v || !k_stride || !v_stride || !kp || !vp) return fail(VB_ERR_INVALID, "vb_pool_kv: null argument");
+  if ((k_r == nullptr) != (v_r == nullptr)) return fail(VB_ERR_INVALID, "vb_pool_kv: give both k_r and v_r or neither");
   if (B <= 0 || H <= 0 || L <= 0 || gap <= 0 || D % 8) return fail(VB_ERR_INVALID, "vb_pool_kv: bad sizes");
   for (int i = 0; i < 3; ++i)
     if ((k_stride[i] | v_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_pool_kv: strides must be multiples of 8");
@@ -419,11 +506,13 @@ extern "C" int vb_pool_kv(const void* k, const void* v, const int64_t* k_stride,
   if (dtype == VB_DTYPE_BF16)
     hipLaunchKernelGGL(pool_kv_kernel<BF16>, grid, dim3(256), 0, s, kb, vb_, k_stride[0], k_stride[1], k_stride[2],
                        v_stride[0], v_stride[1], v_stride[2], rows, B, H, L, D, gap, Lp,
-                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp));
+                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp),
+                       reinterpret_cast<uint8_t*>(k_r), reinterpret_cast<uint8_t*>(v_r));
   else if (dtype == VB_DTYPE_F16)
     hipLaunchKernelGGL(pool_kv_kernel<F16>, grid, dim3(256), 0, s, kb, vb_, k_stride[0], k_stride[1], k_stride[2],
                        v_stride[0], v_stride[1], v_stride[2], rows, B, H, L, D, gap, Lp,
-                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp));
+                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp),
+                       reinterpret_cast<uint8_t*>(k_r), reinterpret_cast<uint8_t*>(v_r));
   else
     return fail(VB_ERR_INVALID, "vb_pool_kv: unknown dtype");
   return check_launch("pool_kv_kernel");

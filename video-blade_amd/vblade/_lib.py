@@ -36,6 +36,7 @@ class AttnArgs(ctypes.Structure):
         ("D", ctypes.c_int),
         ("scale", ctypes.c_float),
         ("dtype", ctypes.c_int),
+        ("heavy_rows", ctypes.c_int),
     ]
 
 
@@ -71,7 +72,7 @@ SIGNATURES = {
         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
     "vb_pool_kv": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-        ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
+        ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     "vb_lse_combine": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_float, ctypes.c_int, _vp, _vp, _vp]),

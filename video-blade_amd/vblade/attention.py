@@ -208,9 +208,12 @@ class AdaptiveBlockSparseAttn(nn.Module):
             from .autograd import adaptive_split_attention
             out = adaptive_split_attention(q, k, v, mask, rows, self.sample_gap)
         else:
-            kp, vp = ops.pool_kv(k, v, self.sample_gap, rows)
-            out = ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kv_rows=rows, kp=kp,
-                                    vp=vp, kp_log_bias=math.log(self.sample_gap))
+            # one pass over K/V: pooled K/V + Gilbert-ordered contiguous copies the attention
+            # kernel streams by LDS-DMA; q rows gathered and out rows scattered in the kernel
+            kp, vp, k_r, v_r = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True)
+            out = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
+                                    kp_log_bias=math.log(self.sample_gap),
+                                    heavy_rows=self.force_tail)
         if self.log_every and self.sparsity_counter % self.log_every == 0:
             print(f"sparsity: {self.sparsity}")
         return out

@@ -55,9 +55,9 @@ def block_sparse_attn_func(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k
 class _AdaptiveSplitFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, mask, rows, gap):
-        out1, lse1 = ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kv_rows=rows,
-                                       need_lse=True)
-        kp, vp = ops.pool_kv(k, v, gap, rows)
+        kp, vp, k_r, v_r = ops.pool_kv(k, v, gap, rows, reordered=True)
+        out1, lse1 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,
+                                       heavy_rows=2)
         out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
                                        need_lse=True)
         out, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)

@@ -88,7 +88,7 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
                   kv_rows: Optional[torch.Tensor] = None, kp: Optional[torch.Tensor] = None,
                   vp: Optional[torch.Tensor] = None, kp_log_bias: float = 0.0, use_main: bool = True,
                   scale: Optional[float] = None, need_lse: bool = False,
-                  out: Optional[torch.Tensor] = None):
+                  out: Optional[torch.Tensor] = None, heavy_rows: int = 0):
     """vb_attn_fwd: softmax over (block-masked keys of k/v) ∪ (pooled keys kp/vp + bias).
     q,k,v [B,H,L,D]; block_mask [B,H,ceil(Lq/128),ceil(Lk/128)] bool/uint8; rows int32.
     Returns out [B,H,Lq,D] (and lse fp32 [B,H,Lq] when need_lse)."""
@@ -135,6 +135,7 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
     a.B, a.H, a.Lq, a.Lk, a.D = B, H, Lq, Lk, D
     a.scale = float(scale) if scale else 0.0
     a.dtype = _dtype_code(q)
+    a.heavy_rows = int(heavy_rows)
     check(_lib.load().vb_attn_fwd(ctypes.byref(a), _stream(dev)), "vb_attn_fwd")
     return (out, lse) if need_lse else out
 
@@ -214,18 +215,24 @@ def energy_mask(po, *, energy_threshold=0.95, min_keep=1, max_keep=1, force_tail
     return mask
 
 
-def pool_kv(k, v, gap: int, rows=None):
-    """vb_pool_kv: mean over `gap` consecutive reordered tokens (replicate pad) -> kp, vp."""
+def pool_kv(k, v, gap: int, rows=None, reordered: bool = False):
+    """vb_pool_kv: mean over `gap` consecutive reordered tokens (replicate pad) -> kp, vp; with
+    reordered=True also returns the Gilbert-ordered contiguous copies (k_r, v_r) written in the
+    same pass."""
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
     B, H, L, D = k.shape
     Lp = (L + gap - 1) // gap
     kp = torch.empty(B, H, Lp, D, device=dev, dtype=k.dtype)
     vp = torch.empty(B, H, Lp, D, device=dev, dtype=v.dtype)
+    k_r = torch.empty(B, H, L, D, device=dev, dtype=k.dtype) if reordered else None
+    v_r = torch.empty(B, H, L, D, device=dev, dtype=v.dtype) if reordered else None
     check(_lib.load().vb_pool_kv(k.data_ptr(), v.data_ptr(), ctypes.cast(_s3(k), ctypes.c_void_p),
                                  ctypes.cast(_s3(v), ctypes.c_void_p), _ptr(rows), B, H, L, D,
                                  int(gap), _dtype_code(k), kp.data_ptr(), vp.data_ptr(),
-                                 _stream(dev)), "vb_pool_kv")
+                                 _ptr(k_r), _ptr(v_r), _stream(dev)), "vb_pool_kv")
+    if reordered:
+        return kp, vp, k_r, v_r
     return kp, vp
 
 
