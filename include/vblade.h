@@ -154,6 +154,61 @@ int vb_lse_combine(const void* out1, const float* lse1, const void* out2, const 
                    int B, int H, int L, int D, float gap, int dtype, void* out, float* alpha,
                    void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Backward (FlashAttention-2 semantics, deterministic: no atomics) of the block-sparse attention
+ * and of the adaptive module's two-branch form, as the reference's autograd computes it
+ * (cogvideo_blocksparseattn.py:316-320 + :366-393):
+ *   main branch   keys k/v [B,H,Lk,D] in REORDERED order (row g = reordered key g), block_mask
+ *                 [B,H,ceil(Lq/128),ceil(Lk/128)] (NULL = dense), its output `out` and LSE `lse`
+ *   pooled branch (kp != NULL) kp/vp [B,H,Lkp,D], its output out2 and LSE lse2 (no bias), the
+ *                 combine weight alpha (fp32 [B,H,Lq], as vb_lse_combine writes it) — LSEs and alpha
+ *                 are constants: dO1 = alpha*dO, dO2 = storage(1-alpha)*dO; the pooled K/V grads
+ *                 are folded back through the mean pool over `pool_gap` reordered keys (replicate
+ *                 padding onto the last key)
+ * q/out/out2/dout/lse/lse2/alpha/dq rows are addressed through q_rows[g] like vb_attn_fwd; dk/dv of
+ * reordered key g are written at row kv_rows[g] (NULL = g). dq/dk/dv are fully overwritten.
+ * `workspace` (device, 16-byte aligned) of at least vb_attn_bwd_workspace_size(args) bytes.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vb_attn_bwd_args {
+  const void* q; int64_t q_stride[3];
+  const void* k; const void* v; int64_t k_stride[3]; int64_t v_stride[3];
+  const int32_t* q_rows;    /* [Lq] or NULL */
+  const int32_t* kv_rows;   /* [Lk] or NULL */
+  const uint8_t* block_mask; int64_t mask_stride[3];
+  const void* out; int64_t out_stride[3];
+  const float* lse;         /* [B,H,Lq] natural log */
+  const void* kp; const void* vp; int64_t kp_stride[3]; int64_t vp_stride[3];
+  int Lkp;
+  const void* out2; int64_t out2_stride[3];
+  const float* lse2;        /* [B,H,Lq] */
+  const float* alpha;       /* [B,H,Lq] or NULL (= 1: no pooled branch) */
+  int pool_gap;
+  const void* dout; int64_t dout_stride[3];
+  void* dq; int64_t dq_stride[3];
+  void* dk; void* dv; int64_t dk_stride[3]; int64_t dv_stride[3];
+  void* workspace; uint64_t workspace_bytes;
+  int B, H, Lq, Lk, D;
+  float scale;              /* <= 0 -> D^-1/2 */
+  int dtype;
+  int heavy_rows;           /* scheduling hint as in vb_attn_args */
+} vb_attn_bwd_args;
+uint64_t vb_attn_bwd_workspace_size(const vb_attn_bwd_args* args);
+int vb_attn_bwd(const vb_attn_bwd_args* args, void* stream);
+
+/* Drop-in for the block_sparse_attn_func backward (same tensor conventions as
+ * vb_block_sparse_attn_fwd): dq/dk/dv [total, H, D]; softmax_lse as the forward wrote it.
+ * workspace >= vb_block_sparse_attn_bwd_workspace_size(batch, num_heads, max_seqlen_q) bytes. */
+uint64_t vb_block_sparse_attn_bwd_workspace_size(int batch, int num_heads, int max_seqlen_q);
+int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, const void* k_unpad,
+                             const void* v_unpad, const void* out_unpad, const float* softmax_lse,
+                             const int32_t* cu_seqlens_q, const int32_t* cu_seqlens_k,
+                             const int32_t* head_mask_type, const int32_t* streaming_info,
+                             const uint8_t* base_blockmask, int batch, int num_heads, int head_dim,
+                             int max_seqlen_q, int max_seqlen_k, float p_dropout, float softmax_scale,
+                             int is_causal, int exact_streaming, int deterministic, int dtype,
+                             void* dq, void* dk, void* dv, void* workspace, uint64_t workspace_bytes,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

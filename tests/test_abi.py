@@ -43,9 +43,10 @@ def test_abi_version(lib):
 
 def test_struct_layouts_match_header():
     """sizeof/offsetof of vb_attn_args and vb_predict_args from gcc == the ctypes mirrors."""
-    from vblade._lib import AttnArgs, PredictArgs
-    fields = {"vb_attn_args": [f[0] for f in AttnArgs._fields_],
-              "vb_predict_args": [f[0] for f in PredictArgs._fields_]}
+    from vblade._lib import AttnArgs, BwdArgs, PredictArgs
+    structs = (("vb_attn_args", AttnArgs), ("vb_predict_args", PredictArgs),
+               ("vb_attn_bwd_args", BwdArgs))
+    fields = {st: [f[0] for f in cls._fields_] for st, cls in structs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for st, fl in fields.items():
         lines.append(f'printf("{st} %zu\\n", sizeof({st}));')
@@ -59,7 +60,7 @@ def test_struct_layouts_match_header():
         subprocess.check_call(["gcc", "-std=c99", c, "-o", exe])
         out = subprocess.check_output([exe]).decode().split("\n")
     got = dict(line.split() for line in out if line)
-    for st, cls in (("vb_attn_args", AttnArgs), ("vb_predict_args", PredictArgs)):
+    for st, cls in structs:
         assert int(got[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
             assert int(got[f"{st}.{f}"]) == getattr(cls, f).offset, f"{st}.{f}"
@@ -92,6 +93,20 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     assert lib.vb_energy_mask(None, 1, 1, 1, 1, 0.95, 1, 1, 0, 0, None, None, None) == _lib.VB_ERR_INVALID
     assert lib.vb_pool_kv(None, None, None, None, None, 1, 1, 1, 64, 15, 0, None, None, None, None, None) == _lib.VB_ERR_INVALID
     assert lib.vb_lse_combine(None, None, None, None, 1, 1, 1, 64, 15.0, 0, None, None, None) == _lib.VB_ERR_INVALID
+    b = _lib.BwdArgs()
+    assert lib.vb_attn_bwd(ctypes.byref(b), None) == _lib.VB_ERR_INVALID
+    b.B = b.H = 1
+    b.Lq = b.Lk = 128
+    b.D = 96
+    assert lib.vb_attn_bwd(ctypes.byref(b), None) == _lib.VB_ERR_UNSUPPORTED
+    assert b"head_dim" in lib.vb_last_error()
+    # workspace sizing is pure host arithmetic
+    b.D = 64
+    assert lib.vb_attn_bwd_workspace_size(ctypes.byref(b)) >= 2 * 64 * 4 * 4
+    assert lib.vb_block_sparse_attn_bwd_workspace_size(1, 1, 128) > 0
+    rc = lib.vb_block_sparse_attn_bwd(*([None] * 11), 1, 1, 64, 128, 128, 0.1, 0.0, 0, 0, 1, 0,
+                                      None, None, None, None, 0, None)
+    assert rc == _lib.VB_ERR_UNSUPPORTED and b"dropout" in lib.vb_last_error()
 
 
 def test_ops_refuse_cpu_tensors():
@@ -101,6 +116,9 @@ def test_ops_refuse_cpu_tensors():
     q = torch.zeros(1, 1, 128, 64, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError, match="HIP"):
         ops.attention_fwd(q, q, q)
+    lse = torch.zeros(1, 1, 128)
+    with pytest.raises(RuntimeError, match="HIP"):
+        ops.attention_bwd(q, q, q, q, q, lse)
 
 
 def test_module_config_and_retain_counts():

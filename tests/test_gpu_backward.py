@@ -1,0 +1,196 @@
+"""GPU parity of the backward kernels (vb_attn_bwd / vb_block_sparse_attn_bwd, through the C ABI)
+against the oracle's FlashAttention-2-semantics backward (oracle/bsa_oracle.py, fp64) on the same
+inputs and the same forward statistics (out, lse).
+
+Tolerance: relative Frobenius error ||g - g_ref|| / ||g_ref|| <= 2e-2 per gradient. The kernels
+feed P and dS to the MFMAs in the storage dtype (as the reference library's backward does) and
+accumulate in fp32; the oracle keeps everything in fp64 — bf16 rounding of P/dS alone gives
+errors of ~4e-3 relative.
+"""
+import math
+
+import pytest
+import torch
+
+import bsa_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 2e-2
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import vblade
+    vblade.load_library()
+
+
+def _rand(*shape, dtype=torch.bfloat16, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+def rel(x, ref):
+    ref = ref.double()
+    return ((x.double().cpu() - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
+def _ops():
+    from vblade import ops
+    return ops
+
+
+@pytest.mark.parametrize("L,D,dtype,density", [(300, 64, torch.bfloat16, 0.5),
+                                               (256, 128, torch.bfloat16, 1.0),
+                                               (517, 64, torch.float16, 0.3),
+                                               (260, 128, torch.bfloat16, 0.6),
+                                               (1000, 64, torch.bfloat16, 0.25)])
+def test_block_sparse_bwd_matches_oracle(L, D, dtype, density):
+    B, H = 1, 2
+    q, k, v, do = (_rand(B, H, L, D, dtype=dtype, seed=s) for s in range(4))
+    nb = (L + 127) // 128
+    mask = O.block_mask_from_density(B, H, nb, nb, density, seed=7)
+    ops = _ops()
+    out, lse = ops.attention_fwd(q.to(DEV), k.to(DEV), v.to(DEV), block_mask=mask.to(DEV),
+                                 need_lse=True)
+    dq, dk, dv = ops.attention_bwd(do.to(DEV), q.to(DEV), k.to(DEV), v.to(DEV), out, lse,
+                                   block_mask=mask.to(DEV))
+    rq, rk, rv = O.block_sparse_attention_bwd(q, k, v, out.cpu(), lse.cpu(), do, mask)
+    for name, g, r in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
+        assert torch.isfinite(g).all(), name
+        assert rel(g, r) <= TOL, (name, rel(g, r))
+
+
+def test_bwd_empty_rows_and_columns_and_determinism():
+    """A q-block row with no kept block (lse = -inf, out = 0) gets dq = 0 and contributes nothing;
+    a key block kept by no row gets dk = dv = 0. Two runs are bitwise identical (no atomics)."""
+    B, H, L, D = 1, 2, 384, 64
+    q, k, v, do = (_rand(B, H, L, D, seed=10 + s) for s in range(4))
+    mask = O.block_mask_from_density(B, H, 3, 3, 0.6, seed=2)
+    mask[:, 0, 1, :] = False      # head 0: q-block 1 keeps nothing
+    mask[:, 1, :, 2] = False      # head 1: key block 2 kept by nobody
+    ops = _ops()
+    qd, kd, vd, dod, md = (t.to(DEV) for t in (q, k, v, do, mask))
+    out, lse = ops.attention_fwd(qd, kd, vd, block_mask=md, need_lse=True)
+    g1 = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
+    g2 = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+    dq, dk, dv = (t.float().cpu() for t in g1)
+    assert torch.isfinite(dq).all() and torch.isfinite(dk).all() and torch.isfinite(dv).all()
+    assert dq[0, 0, 128:256].abs().max() == 0
+    assert dk[0, 1, 256:].abs().max() == 0 and dv[0, 1, 256:].abs().max() == 0
+    lse_c = lse.cpu().clone()
+    lse_c[torch.isinf(lse_c)] = float("inf")   # oracle: P = exp(-inf - inf) = 0 on empty rows
+    rq, rk, rv = O.block_sparse_attention_bwd(q, k, v, out.cpu(), lse_c, do, mask)
+    for g, r in ((dq, rq), (dk, rk), (dv, rv)):
+        assert rel(g, r) <= TOL
+
+
+def test_block_sparse_attn_func_autograd_varlen():
+    """Reference-API drop-in (block_sparse_attn_func, varlen layout, head_mask_type = ones ->
+    per-head masks) differentiated by torch.autograd, per sequence against the oracle."""
+    import vblade
+    H, D = 2, 64
+    lens = [300, 170]
+    tot = sum(lens)
+    q, k, v, do = (_rand(tot, H, D, seed=20 + s) for s in range(4))
+    cu = torch.tensor([0, lens[0], tot], dtype=torch.int32)
+    nb = (max(lens) + 127) // 128
+    mask = O.block_mask_from_density(2, H, nb, nb, 0.5, seed=4)
+    qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+    out = vblade.block_sparse_attn_func(qd, kd, vd, cu.to(DEV), cu.to(DEV),
+                                        torch.ones(H, dtype=torch.int32, device=DEV), None,
+                                        mask.to(DEV), max(lens), max(lens), 0.0,
+                                        deterministic=True)
+    out.backward(do.to(DEV))
+    for bi, Lb in enumerate(lens):
+        s0 = int(cu[bi])
+        sl = lambda t: t[s0:s0 + Lb].permute(1, 0, 2)[None].float()  # noqa: E731
+        nbb = (Lb + 127) // 128
+        mb = mask[bi:bi + 1, :, :nbb, :nbb]
+        ro, rlse = O.block_sparse_attention(sl(q), sl(k), sl(v), mb)
+        rq, rk, rv = O.block_sparse_attention_bwd(sl(q), sl(k), sl(v), sl(out.detach().cpu()),
+                                                  rlse, sl(do), mb)
+        assert rel(sl(out.detach().cpu()), ro) <= TOL
+        for g, r in ((qd.grad, rq), (kd.grad, rk), (vd.grad, rv)):
+            assert rel(sl(g.cpu()), r) <= TOL
+
+
+def _small_module(variant):
+    import vblade
+    if variant == "cog":
+        kw = dict(width=12, height=8, depth=5, text_length=40, sample_gap=15,
+                  min_retain_ratio=0.4, max_retain_ratio=0.6)
+        cfg = O.AdaptiveConfig.cogvideox(width=12, height=8, depth=5, text_length=40,
+                                         sample_gap=15, min_retain_ratio=0.4, max_retain_ratio=0.6)
+    else:
+        kw = dict(width=10, height=6, depth=6, sample_gap=30, min_retain_ratio=0.3,
+                  max_retain_ratio=0.6)
+        cfg = O.AdaptiveConfig.wan(width=10, height=6, depth=6, sample_gap=30,
+                                   min_retain_ratio=0.3, max_retain_ratio=0.6)
+    return vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **kw), cfg
+
+
+def _realistic(B, H, L, D, seed):
+    g = torch.Generator().manual_seed(seed)
+    cent = torch.randn(B, H, L // 128 + 1, D, generator=g).repeat_interleave(128, 2)[:, :, :L]
+    q = (torch.randn(B, H, L, D, generator=g) + 2 * cent).to(torch.bfloat16)
+    k = (torch.randn(B, H, L, D, generator=g) + 2 * cent).to(torch.bfloat16)
+    v = torch.randn(B, H, L, D, generator=g).to(torch.bfloat16)
+    do = torch.randn(B, H, L, D, generator=g).to(torch.bfloat16)
+    return q, k, v, do
+
+
+def _check_adaptive_grads(m, cfg, q, k, v, do):
+    qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+    out = m(qd, kd, vd)
+    out.backward(do.to(DEV))
+    mask = m.last_mask.bool().cpu()
+    fwd = O.adaptive_attention(q, k, v, cfg, None, None, mask=mask)
+    assert rel(out.detach().float().cpu(), fwd["out"]) <= TOL
+    rq, rk, rv = O.adaptive_attention_bwd(q, k, v, do, cfg, fwd)
+    for name, g, r in (("dq", qd.grad, rq), ("dk", kd.grad, rk), ("dv", vd.grad, rv)):
+        assert torch.isfinite(g).all(), name
+        assert rel(g, r) <= TOL, (name, rel(g, r))
+
+
+@pytest.mark.parametrize("variant,H,D", [("cog", 2, 64), ("wan", 2, 128)])
+def test_adaptive_module_backward_matches_oracle(variant, H, D):
+    """Training path (grad enabled): the reference's two-branch autograd — alpha detached,
+    pooled-branch K/V grads through the mean pool, Gilbert gather transposed."""
+    m, cfg = _small_module(variant)
+    L = m.gilbert_rearranger.seq_len
+    q, k, v, do = _realistic(1, H, L, D, seed=3)
+    _check_adaptive_grads(m, cfg, q, k, v, do)
+
+
+@pytest.mark.parametrize("variant,D", [("cog", 64), ("wan", 128)])
+def test_full_size_adaptive_backward_one_head(variant, D):
+    """Full CogVideoX (L=17776) / Wan (L=32760) sequence, one head, reference retain ratios."""
+    import vblade
+    m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+    cfg = O.AdaptiveConfig.cogvideox() if variant == "cog" else O.AdaptiveConfig.wan()
+    L = m.gilbert_rearranger.seq_len
+    q, k, v, do = _realistic(1, 1, L, D, seed=5)
+    _check_adaptive_grads(m, cfg, q, k, v, do)
+
+
+def test_training_batch_b2_matches_per_sample():
+    """B=2 (training batches are B=5 in the reference): each sample's grads equal the B=1 grads."""
+    m, cfg = _small_module("cog")
+    L = m.gilbert_rearranger.seq_len
+    q, k, v, do = _realistic(2, 2, L, 64, seed=8)
+    qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+    out = m(qd, kd, vd)
+    out.backward(do.to(DEV))
+    mask_model = m.last_mask
+    for b in range(2):
+        qb, kb, vb = (t[b:b + 1].to(DEV).requires_grad_(True) for t in (q, k, v))
+        ob = m(qb, kb, vb, block_mask=mask_model[b:b + 1])
+        ob.backward(do[b:b + 1].to(DEV))
+        assert math.isclose(rel(qb.grad, qd.grad[b:b + 1].cpu()), 0.0, abs_tol=1e-6)
+        assert math.isclose(rel(kb.grad, kd.grad[b:b + 1].cpu()), 0.0, abs_tol=1e-6)
+        assert math.isclose(rel(vb.grad, vd.grad[b:b + 1].cpu()), 0.0, abs_tol=1e-6)

@@ -58,13 +58,42 @@ def run(variant, density=None):
           f"speedup={t_dense / t_call:.2f}x", flush=True)
 
 
+def run_bwd(variant):
+    """Training-path backward: the two-branch forward's saved tensors -> vb_attn_bwd."""
+    H, D = (48, 64) if variant == "cog" else (12, 128)
+    m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+    L = m.gilbert_rearranger.seq_len
+    dev = torch.device("cuda")
+    q, k, v = realistic_qkv(H, L, D, 0, dev)
+    do = torch.randn_like(q)
+    rows = m._rows(dev)
+    _, mask = m.predict_mask(q, k)
+    gap = m.sample_gap
+    kp, vp, k_r, v_r = ops.pool_kv(k, v, gap, rows, reordered=True)
+    out1, lse1 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,
+                                   heavy_rows=m.force_tail)
+    out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
+                                   need_lse=True)
+    out, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
+    fb = lambda: ops.attention_bwd(do, q, k_r, v_r, out1, lse1, block_mask=mask, q_rows=rows,  # noqa
+                                   kv_rows=rows, kp=kp, vp=vp, out2=out2, lse2=lse2, alpha=alpha,
+                                   gap=gap, heavy_rows=m.force_tail)
+    t_bwd = timeit(fb, reps=5)
+    fl = 2.5 * attn_flops(mask, L, D, kp.shape[2])
+    print(f"{variant} bwd density={mask.float().mean().item():.3f} bwd={t_bwd:.3f}ms "
+          f"({fl / t_bwd / 1e9:.0f} TF/s at 2.5x fwd FLOPs)", flush=True)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--variant", default="both")
     ap.add_argument("--densities", default="")
+    ap.add_argument("--bwd", action="store_true")
     a = ap.parse_args()
     with torch.no_grad():
         for var in (["cog", "wan"] if a.variant == "both" else [a.variant]):
             run(var)
             for d in [float(x) for x in a.densities.split(",") if x]:
                 run(var, d)
+            if a.bwd:
+                run_bwd(var)

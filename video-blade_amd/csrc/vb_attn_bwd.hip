@@ -1,0 +1,841 @@
+// Block-sparse FMHA backward for gfx950 (MI355X): FlashAttention-2 gradient semantics, deterministic.
+//
+// Replaces the backward of the external block_sparse_attn_func (mit-han-lab/Block-Sparse-Attention)
+// as the reference's autograd reaches it (cogvideox/train/special_attentions_local/TrainRelated/
+// cogvideo_blocksparseattn.py:316-320 sparse call, :106-109 dense pooled call) together with the
+// autograd of the surrounding adaptive_block_sparse_attn ops (:366-393):
+//   * the softmax LSE is a constant (the library's backward ignores its gradient), hence the combine
+//     weight a = exp(lse1 - M)/(...) is a constant too: dO1 = a*dO, dO2 = (1-a)*dO;
+//   * each branch back-propagates with its own output and LSE;
+//   * pooled-branch K/V gradients flow back through the mean pool (replicate padding folds onto the
+//     last token) and the Gilbert gather (a scatter to the caller's rows).
+// The branch weight is folded into the row statistic: a*P1 = exp2(S*c - (lse1*log2e - log2 a)),
+// so dO itself is used unscaled and Delta = rowsum(dO * O_branch) (FA2's D_i) per branch.
+//
+// Kernels (all 256 threads = 4 waves, v_mfma_f32_32x32x16, operand maps in vb_tiles.hpp):
+//   bwd_prep_kernel   per row: Delta1/2, L'1/2 -> stats [B*H][ntile64][4][64] fp32; optional
+//                     reordered contiguous copies of q and dO (one gather pass instead of one per
+//                     key block that reads them)
+//   bwd_dkdv_kernel   one workgroup per (b, h, 128-key block); wave = 32 keys held in registers;
+//                     streams the 64-row Q / dO tiles of every q-block that keeps this key block
+//                     (mask column; all q-blocks for pooled keys) through LDS by LDS-DMA:
+//                       S = Q.K^T, dP = dO.V^T         (C: lane = key, registers = q rows)
+//                       P = exp2(S c - L'), dS = P (dP - Delta)
+//                       dV^T += dO^T.P, dK^T += Q^T.dS (A = ds_read_b64_tr_b16 of the Q/dO tiles)
+//                     pooled keys -> fp32 workspace; full-resolution keys -> dk/dv rows (kv_rows),
+//                     adding the mean-pool adjoint of the pooled grads
+//   bwd_dq_kernel     one workgroup per (b, h, 128-row q-block), the forward's geometry: streams the
+//                     kept K/V tiles then the pooled ones:
+//                       S^T = K.Q^T, dP^T = V.dO^T      (C: lane = query, registers = keys)
+//                       dQ^T += K^T.dS^T                (A = transposed read of the K tile)
+// No atomics: every gradient element is written by exactly one workgroup, so results are
+// bit-reproducible run to run (the reference's deterministic=True).
+#include <cstdlib>
+
+#include "vb_tiles.hpp"
+
+namespace vb {
+
+namespace bwd {
+constexpr int kThreads = 256;
+constexpr int kBlk = 128;       // mask block (rows and keys)
+constexpr int kT = 64;          // rows (dkdv) / keys (dq) per LDS tile
+constexpr int kMaxBlocks = 1024;
+constexpr float kBigL = 1.0e30f;  // L' of rows that must contribute nothing (exp2(s - 1e30) = 0)
+}  // namespace bwd
+
+struct PrepParams {
+  const void* q; const void* dout; const void* out; const void* out2;
+  int64_t qs[3], dos[3], os[3], o2s[3];
+  const float* lse; const float* lse2; const float* alpha;  // [B,H,Lq] at the caller's row
+  const int32_t* q_rows; const int32_t* cu_q;
+  void* q_r; void* do_r;  // [B,H,Lq,D] contiguous reordered copies (written when q_rows != NULL)
+  float* stats;           // [B*H][ntile][4][64]: L'1, Delta1, L'2, Delta2
+  int B, H, Lq, D, ntile;
+};
+
+struct BwdParams {
+  const void* q; const void* dout; int64_t qs[3], dos[3];  // row g of (b,h) at qrow0 + g
+  const void* k; const void* v; int64_t ks[3], vs[3];
+  const void* kp; const void* vp; int64_t kps[3], vps[3];
+  int Lkp;
+  const int32_t* cu_q; const int32_t* cu_k; const int32_t* head_mask_type;
+  const uint8_t* mask; int64_t ms[3];
+  const float* stats; int ntile;
+  void* dq; int64_t dqs[3]; const int32_t* q_rows;
+  void* dk; void* dv; int64_t dks[3], dvs[3]; const int32_t* kv_rows;
+  float* dkp; float* dvp;  // [B,H,Lkp,D] fp32 pooled-key grads
+  int gap;
+  int B, H, Lq, Lk, nbq, nbk, nbkp;
+  float c;      // scale * log2(e)
+  float scale;
+  int heavy_rows;
+};
+
+// ------------------------------------------------------------------------------------------------
+// prep: one thread per 16-byte chunk of a row
+// ------------------------------------------------------------------------------------------------
+template <class T>
+__global__ void __launch_bounds__(256) bwd_prep_kernel(const PrepParams p) {
+  const int CH = p.D / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t rows_per_bh = (int64_t)p.ntile * 64;
+  const int64_t total = (int64_t)p.B * p.H * rows_per_bh * CH;
+  if (idx >= total) return;  // CH divides 64: whole row groups leave together
+  const int ch = idx % CH;
+  const int64_t rid = idx / CH;
+  const int g = rid % rows_per_bh;
+  const int bh = rid / rows_per_bh;
+  const int b = bh / p.H, h = bh % p.H;
+  int Lq = p.Lq, qrow0 = 0;
+  if (p.cu_q) { qrow0 = p.cu_q[b]; Lq = p.cu_q[b + 1] - qrow0; }
+  const bool valid = g < Lq;
+  const int row = valid ? (p.q_rows ? p.q_rows[g] : g) : 0;
+  float d1 = 0.f, d2 = 0.f;
+  if (valid) {
+    const int64_t r = qrow0 + row;
+    const u32x4 dov = *reinterpret_cast<const u32x4*>(
+        reinterpret_cast<const uint8_t*>(p.dout) + 2 * (b * p.dos[0] + h * p.dos[1] + r * p.dos[2] + ch * 8));
+    const u32x4 ov = *reinterpret_cast<const u32x4*>(
+        reinterpret_cast<const uint8_t*>(p.out) + 2 * (b * p.os[0] + h * p.os[1] + r * p.os[2] + ch * 8));
+    u32x4 o2v = {0, 0, 0, 0};
+    if (p.out2)
+      o2v = *reinterpret_cast<const u32x4*>(
+          reinterpret_cast<const uint8_t*>(p.out2) + 2 * (b * p.o2s[0] + h * p.o2s[1] + r * p.o2s[2] + ch * 8));
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float x = T::bits_to_f32((dov[e] >> (16 * s)) & 0xffff);
+        d1 += x * T::bits_to_f32((ov[e] >> (16 * s)) & 0xffff);
+        d2 += x * T::bits_to_f32((o2v[e] >> (16 * s)) & 0xffff);
+      }
+    if (p.q_r) {
+      const u32x4 qv = *reinterpret_cast<const u32x4*>(
+          reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + r * p.qs[2] + ch * 8));
+      const int64_t dst = 2 * (((int64_t)bh * p.Lq + g) * p.D + ch * 8);
+      *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(p.q_r) + dst) = qv;
+      *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(p.do_r) + dst) = dov;
+    }
+  }
+  // reduce over the CH consecutive lanes of this row (CH in {8, 16}, aligned groups)
+  for (int o = 1; o < CH; o <<= 1) {
+    d1 += __shfl_xor(d1, o);
+    d2 += __shfl_xor(d2, o);
+  }
+  if (ch != 0) return;
+  float l1 = bwd::kBigL, l2 = bwd::kBigL;
+  if (valid) {
+    const int64_t li = (int64_t)bh * p.Lq + row;
+    const float a = p.alpha ? p.alpha[li] : 1.f;
+    const float lse1 = p.lse[li];
+    // a * P1 = exp2(S c - (lse1 log2e - log2 a)); rows with no kept key (lse = -inf) or a = 0
+    // contribute nothing
+    if (lse1 > -INFINITY && a > 0.f) l1 = fminf(lse1 * kLog2e - __log2f(a), bwd::kBigL);
+    if (p.lse2) {
+      const float w2 = round_to<T>(1.f - a);  // the reference's bf16 (1 - alpha), :393
+      const float lse2 = p.lse2[li];
+      if (lse2 > -INFINITY && w2 > 0.f) l2 = fminf(lse2 * kLog2e - __log2f(w2), bwd::kBigL);
+    }
+  } else {
+    d1 = d2 = 0.f;
+  }
+  float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
+  st[0] = l1;
+  st[64] = d1;
+  st[128] = l2;
+  st[192] = d2;
+}
+
+// ------------------------------------------------------------------------------------------------
+// dK / dV: one workgroup per (b, h, 128-key block)
+// ------------------------------------------------------------------------------------------------
+template <int D, class T, bool kPooled>
+__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kernel(const BwdParams p) {
+  using namespace bwd;
+  constexpr int KS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int RB = D * 2;                 // bytes per row
+  constexpr int kTileBytes = kT * RB;       // one 64-row Q (or dO) tile
+  constexpr int kInstTile = kTileBytes / 1024;
+  constexpr int kRowsPerInst = 1024 / RB;
+  constexpr int kCh = RB / 16;
+  constexpr int kInst = 2 * kInstTile + 1;  // Q, dO, stats (1 KiB)
+  constexpr int kBufBytes = 2 * kTileBytes + 1024;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBufBytes + kMaxBlocks * 2 + 16];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + 2 * kBufBytes);
+  int* list_n = reinterpret_cast<int*>(smem + 2 * kBufBytes + kMaxBlocks * 2);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+
+  const int BH = p.B * p.H;
+  const int nkb = kPooled ? p.nbkp : p.nbk;
+  // pooled-key blocks see every q-block (long workgroups): plain order; main blocks XCD-contiguous
+  const int lin = kPooled ? (int)blockIdx.x : xcd_linear(blockIdx.x, nkb * BH);
+  const int bh = lin / nkb;
+  const int kblk = lin % nkb;
+  const int b = bh / p.H, h = bh % p.H;
+
+  int Lq = p.Lq, Lk = p.Lk;
+  int64_t qrow0 = 0, krow0 = 0;
+  if (p.cu_q) {
+    qrow0 = p.cu_q[b]; Lq = p.cu_q[b + 1] - p.cu_q[b];
+    krow0 = p.cu_k[b]; Lk = p.cu_k[b + 1] - p.cu_k[b];
+  }
+  const int Lkey = kPooled ? p.Lkp : Lk;
+  const int k0 = kblk * kBlk;
+  if (k0 >= Lkey || Lq <= 0) return;
+  const int nbq = (Lq + kBlk - 1) / kBlk;
+
+  bool nan_head = false;
+  const uint8_t* mcol = nullptr;
+  if (!kPooled) {
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
+    if (mh) mcol = mh + kblk;
+  }
+  if (threadIdx.x < 64) {
+    int n = 0;
+    for (int i0 = 0; i0 < nbq; i0 += 64) {
+      const int i = i0 + lane;
+      const bool keep = (i < nbq) && (mcol == nullptr || mcol[(int64_t)i * p.ms[2]] != 0);
+      const unsigned long long bal = __ballot(keep);
+      if (keep) {
+        const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+        list[pos] = (uint16_t)i;
+      }
+      n += __popcll(bal);
+    }
+    if (lane == 0) *list_n = n;
+  }
+
+  // this wave's 32 keys as B operands (lane = key, d = 16 ks + 8 half + 0..7)
+  const int key = k0 + wave * 32 + l32;
+  const bool kvalid = key < Lkey;
+  const int keyc = kvalid ? key : Lkey - 1;
+  const uint8_t* kb = kPooled
+      ? reinterpret_cast<const uint8_t*>(p.kp) + 2 * (b * p.kps[0] + h * p.kps[1] + (int64_t)keyc * p.kps[2])
+      : reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + (krow0 + keyc) * p.ks[2]);
+  const uint8_t* vb_ = kPooled
+      ? reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1] + (int64_t)keyc * p.vps[2])
+      : reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + (krow0 + keyc) * p.vs[2]);
+  typename T::vec8 kf[KS], vf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = *reinterpret_cast<const typename T::vec8*>(kb + (16 * s + 8 * half) * 2);
+    vf[s] = *reinterpret_cast<const typename T::vec8*>(vb_ + (16 * s + 8 * half) * 2);
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    asm volatile("" : "+v"(kf[s]));
+    asm volatile("" : "+v"(vf[s]));
+  }
+  __syncthreads();
+  const int nlist = __builtin_amdgcn_readfirstlane(*list_n);
+  int ntiles = 2 * nlist;
+  if (nlist > 0 && list[nlist - 1] == nbq - 1 && (nbq - 1) * kBlk + kT >= Lq) ntiles -= 1;
+
+  const uint8_t* qsrc = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + qrow0 * p.qs[2]);
+  const uint8_t* dosrc = reinterpret_cast<const uint8_t*>(p.dout) + 2 * (b * p.dos[0] + h * p.dos[1] + qrow0 * p.dos[2]);
+  const int64_t qstride = 2 * p.qs[2], dostride = 2 * p.dos[2];
+  const float* stsrc = p.stats + (int64_t)bh * p.ntile * 256;
+
+  // DMA of tile t (64 q rows) into buffer t & 1: instruction i -> Q (i < kInstTile), dO, stats.
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    const int qb = __builtin_amdgcn_readfirstlane(list[t >> 1]);
+    const int row0 = qb * kBlk + (t & 1) * kT;
+    const int nvalid = min(kT, Lq - row0);
+    uint8_t* buf = smem + (t & 1) * kBufBytes;
+    for (int i = wave; i < kInst; i += 4) {
+      const void* src;
+      if (i < 2 * kInstTile) {
+        const int ii = i < kInstTile ? i : i - kInstTile;
+        const int r = ii * kRowsPerInst + lane / kCh;
+        const int c = (lane % kCh) ^ dual_swz<D>(r);
+        const int sr = row0 + min(r, nvalid - 1);
+        src = i < kInstTile ? (const void*)(qsrc + sr * qstride + c * 16)
+                            : (const void*)(dosrc + sr * dostride + c * 16);
+      } else {
+        src = stsrc + (row0 / 64) * 256 + lane * 4;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[i][r] = dv[i][r] = 0.f;
+
+  const int trr = tr_row(lane), trc = tr_col(lane);
+  constexpr int fL = kPooled ? 2 : 0;  // stats fields of this branch
+  constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
+  const bool many = wave < (kInst & 3);
+
+  if (ntiles > 0) issue(0);
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) {
+      issue(t + 1);
+      if (many) VB_WAIT_VMCNT(kHi);
+      else VB_WAIT_VMCNT(kLo);
+    } else {
+      VB_WAIT_VMCNT(0);
+    }
+    __builtin_amdgcn_s_barrier();
+    const uint8_t* qt = smem + (t & 1) * kBufBytes;
+    const uint8_t* dot = qt + kTileBytes;
+    const float* st = reinterpret_cast<const float*>(qt + 2 * kTileBytes);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        s = T::mfma32(lds_b128<T>(qt, dual_off<D>(32 * u + l32, 2 * ks + half)), kf[ks], s);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        dp = T::mfma32(lds_b128<T>(dot, dual_off<D>(32 * u + l32, 2 * ks + half)), vf[ks], dp);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 Lv = *reinterpret_cast<const f32x4*>(st + fL * 64 + 32 * u + 8 * j + 4 * half);
+        const f32x4 Dv = *reinterpret_cast<const f32x4*>(st + (fL + 1) * 64 + 32 * u + 8 * j + 4 * half);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * j + e;
+          const float pr = exp2_fast(fmaf(s[r], p.c, -Lv[e]));
+          s[r] = pr;
+          dp[r] = pr * (dp[r] - Dv[e]);
+        }
+      }
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const typename T::vec8 pp = pack8<T>(s, 8 * sb);
+        const typename T::vec8 pd = pack8<T>(dp, 8 * sb);
+        const int rr = 32 * u + 16 * sb + trr;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          s16x4 dol = lds_tr4(dot, dual_off_col<D>(rr, 32 * dt + trc));
+          s16x4 doh = lds_tr4(dot, dual_off_col<D>(rr + 8, 32 * dt + trc));
+          s16x4 ql = lds_tr4(qt, dual_off_col<D>(rr, 32 * dt + trc));
+          s16x4 qh = lds_tr4(qt, dual_off_col<D>(rr + 8, 32 * dt + trc));
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(dol), "+v"(doh), "+v"(ql), "+v"(qh));
+          dv[dt] = T::mfma32(join8<T>(dol, doh), pp, dv[dt]);
+          dk[dt] = T::mfma32(join8<T>(ql, qh), pd, dk[dt]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_barrier();  // buffer t & 1 is free for tile t + 2
+  }
+
+  // ---- epilogue: lane = key, registers = d ---------------------------------------------------------
+  if (!kvalid) return;
+  const float nanf_ = __builtin_nanf("");
+  if (kPooled) {
+    float* dkr = p.dkp + ((int64_t)bh * p.Lkp + key) * D;
+    float* dvr = p.dvp + ((int64_t)bh * p.Lkp + key) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * half;
+        f32x4 a, c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = dk[dt][4 * g4 + e] * p.scale;
+          c[e] = dv[dt][4 * g4 + e];
+        }
+        *reinterpret_cast<f32x4*>(dkr + d) = a;
+        *reinterpret_cast<f32x4*>(dvr + d) = c;
+      }
+    return;
+  }
+  // full-resolution key: + mean-pool adjoint of the pooled grads (replicate padding folds onto
+  // the last token), written at the caller's row
+  const float* pk = nullptr;
+  const float* pv = nullptr;
+  float pw = 0.f;
+  if (p.dkp) {
+    const int gp = key / p.gap;
+    pk = p.dkp + ((int64_t)bh * p.Lkp + gp) * D;
+    pv = p.dvp + ((int64_t)bh * p.Lkp + gp) * D;
+    const int extra = (key == Lk - 1) ? p.Lkp * p.gap - Lk : 0;
+    pw = (float)(1 + extra) / (float)p.gap;
+  }
+  const int64_t orow = p.kv_rows ? p.kv_rows[key] : krow0 + key;
+  uint8_t* dkr = reinterpret_cast<uint8_t*>(p.dk) + 2 * (b * p.dks[0] + h * p.dks[1] + orow * p.dks[2]);
+  uint8_t* dvr = reinterpret_cast<uint8_t*>(p.dv) + 2 * (b * p.dvs[0] + h * p.dvs[1] + orow * p.dvs[2]);
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * half;
+      float a[4], c[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = dk[dt][4 * g4 + e] * p.scale;
+        c[e] = dv[dt][4 * g4 + e];
+      }
+      if (pk) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(pk + d);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(pv + d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = fmaf(x[e], pw, a[e]);
+          c[e] = fmaf(y[e], pw, c[e]);
+        }
+      }
+      if (nan_head) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = c[e] = nanf_;
+      }
+      u32x2 w, z;
+      w[0] = pack2<T>(a[0], a[1]); w[1] = pack2<T>(a[2], a[3]);
+      z[0] = pack2<T>(c[0], c[1]); z[1] = pack2<T>(c[2], c[3]);
+      *reinterpret_cast<u32x2*>(dkr + d * 2) = w;
+      *reinterpret_cast<u32x2*>(dvr + d * 2) = z;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dQ: one workgroup per (b, h, 128-row q-block); kept full-resolution tiles then pooled tiles
+// ------------------------------------------------------------------------------------------------
+template <int D, class T, bool kPool>
+__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel(const BwdParams p) {
+  using namespace bwd;
+  constexpr int KS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int RB = D * 2;
+  constexpr int kTileBytes = kT * RB;       // one 64-key K (or V) tile
+  constexpr int kInstTile = kTileBytes / 1024;
+  constexpr int kRowsPerInst = 1024 / RB;
+  constexpr int kCh = RB / 16;
+  constexpr int kInst = 2 * kInstTile;
+  constexpr int kBufBytes = 2 * kTileBytes;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBufBytes + kMaxBlocks * 2 + 16];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + 2 * kBufBytes);
+  int* list_n = reinterpret_cast<int*>(smem + 2 * kBufBytes + kMaxBlocks * 2);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+
+  // heavy-first, then XCD-contiguous head-major (as the forward)
+  const int BH = p.B * p.H;
+  const int hr = min(p.heavy_rows, p.nbq);
+  const int n_heavy = hr * BH;
+  int qblk, bh;
+  if ((int)blockIdx.x < n_heavy) {
+    qblk = p.nbq - 1 - (int)(blockIdx.x / BH);
+    bh = blockIdx.x % BH;
+  } else {
+    const int rows_left = p.nbq - hr;
+    const int lin = xcd_linear(blockIdx.x - n_heavy, rows_left * BH);
+    bh = lin / rows_left;
+    qblk = rows_left - 1 - lin % rows_left;
+  }
+  const int b = bh / p.H, h = bh % p.H;
+  int Lq = p.Lq, Lk = p.Lk;
+  int64_t qrow0 = 0, krow0 = 0;
+  if (p.cu_q) {
+    qrow0 = p.cu_q[b]; Lq = p.cu_q[b + 1] - p.cu_q[b];
+    krow0 = p.cu_k[b]; Lk = p.cu_k[b + 1] - p.cu_k[b];
+  }
+  const int q0 = qblk * kBlk;
+  if (q0 >= Lq) return;
+  const int nbk = (Lk + kBlk - 1) / kBlk;
+
+  bool nan_head = false;
+  const uint8_t* mrow = nullptr;
+  const bool use_main = p.k != nullptr;
+  if (use_main) {
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
+    if (mh) mrow = mh + (int64_t)qblk * p.ms[2];
+  }
+  if (threadIdx.x < 64) {
+    int n = 0;
+    if (use_main) {
+      for (int j0 = 0; j0 < nbk; j0 += 64) {
+        const int j = j0 + lane;
+        const bool keep = (j < nbk) && (mrow == nullptr || mrow[j] != 0);
+        const unsigned long long bal = __ballot(keep);
+        if (keep) {
+          const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+          list[pos] = (uint16_t)j;
+        }
+        n += __popcll(bal);
+      }
+    }
+    if (lane == 0) *list_n = n;
+  }
+
+  // this wave's 32 query rows: Q and dO as B operands (lane = query)
+  const int g = q0 + wave * 32 + l32;
+  const bool qvalid = g < Lq;
+  const int gc = qvalid ? g : Lq - 1;
+  typename T::vec8 qf[KS], df[KS];
+  {
+    const uint8_t* qp = reinterpret_cast<const uint8_t*>(p.q) +
+                        2 * (b * p.qs[0] + h * p.qs[1] + (qrow0 + gc) * p.qs[2]);
+    const uint8_t* dp_ = reinterpret_cast<const uint8_t*>(p.dout) +
+                         2 * (b * p.dos[0] + h * p.dos[1] + (qrow0 + gc) * p.dos[2]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
+      df[s] = *reinterpret_cast<const typename T::vec8*>(dp_ + (16 * s + 8 * half) * 2);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      asm volatile("" : "+v"(qf[s]));
+      asm volatile("" : "+v"(df[s]));
+    }
+  }
+  const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
+  float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];
+  asm volatile("" : "+v"(L1), "+v"(D1), "+v"(L2), "+v"(D2));
+  __syncthreads();
+  const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
+  int ntm = 2 * nkept;
+  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kBlk + kT >= Lk) ntm -= 1;
+  const int ntp = kPool ? (p.Lkp + kT - 1) / kT : 0;
+  const int ntiles = ntm + ntp;
+
+  const uint8_t* kbase = use_main ? reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + krow0 * p.ks[2]) : nullptr;
+  const uint8_t* vbase = use_main ? reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + krow0 * p.vs[2]) : nullptr;
+  const uint8_t* kpbase = kPool ? reinterpret_cast<const uint8_t*>(p.kp) + 2 * (b * p.kps[0] + h * p.kps[1]) : nullptr;
+  const uint8_t* vpbase = kPool ? reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1]) : nullptr;
+
+  auto tile_keys = [&](int t, int& kstart, int& klen) __attribute__((always_inline)) {
+    if (t < ntm) {
+      const int blk = __builtin_amdgcn_readfirstlane(list[t >> 1]);
+      kstart = blk * kBlk + (t & 1) * kT;
+      klen = min(kT, Lk - kstart);
+    } else {
+      kstart = (t - ntm) * kT;
+      klen = min(kT, p.Lkp - kstart);
+    }
+  };
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    int kstart, klen;
+    tile_keys(t, kstart, klen);
+    const bool pooled = kPool && t >= ntm;
+    uint8_t* buf = smem + (t & 1) * kBufBytes;
+    for (int i = wave; i < kInst; i += 4) {
+      const bool isv = i >= kInstTile;
+      const int ii = isv ? i - kInstTile : i;
+      const int r = ii * kRowsPerInst + lane / kCh;
+      const int c = (lane % kCh) ^ dual_swz<D>(r);
+      const int64_t key = kstart + min(r, klen - 1);
+      const uint8_t* src;
+      if (pooled) src = isv ? vpbase + key * 2 * p.vps[2] : kpbase + key * 2 * p.kps[2];
+      else src = isv ? vbase + key * 2 * p.vs[2] : kbase + key * 2 * p.ks[2];
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 16),
+                                       (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[i][r] = 0.f;
+  const int trr = tr_row(lane), trc = tr_col(lane);
+  constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
+  const bool many = wave < (kInst & 3);
+
+  if (ntiles > 0) issue(0);
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) {
+      issue(t + 1);
+      if (many) VB_WAIT_VMCNT(kHi);
+      else VB_WAIT_VMCNT(kLo);
+    } else {
+      VB_WAIT_VMCNT(0);
+    }
+    __builtin_amdgcn_s_barrier();
+    int kstart, klen;
+    tile_keys(t, kstart, klen);
+    const bool pooled = kPool && t >= ntm;
+    const float Lr = pooled ? L2 : L1;
+    const float Dr = pooled ? D2 : D1;
+    const uint8_t* kt_ = smem + (t & 1) * kBufBytes;
+    const uint8_t* vt_ = kt_ + kTileBytes;
+    const float nL = -Lr;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {   // 32-key halves: S^T, dP^T -> dS^T -> dQ^T
+      f32x16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        s = T::mfma32(lds_b128<T>(kt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), qf[ks], s);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        dp = T::mfma32(lds_b128<T>(vt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), df[ks], dp);
+      if (klen < kT) {
+        asm volatile("");
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool ok = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half < klen;
+          const float pr = ok ? exp2_fast(fmaf(s[r], p.c, nL)) : 0.f;
+          dp[r] = pr * (dp[r] - Dr);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pr = exp2_fast(fmaf(s[r], p.c, nL));
+          dp[r] = pr * (dp[r] - Dr);
+        }
+      }
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const typename T::vec8 pd = pack8<T>(dp, 8 * sb);
+        const int rr = kt * 32 + 16 * sb + trr;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          s16x4 lo = lds_tr4(kt_, dual_off_col<D>(rr, 32 * dt + trc));
+          s16x4 hi = lds_tr4(kt_, dual_off_col<D>(rr + 8, 32 * dt + trc));
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi));
+          dq[dt] = T::mfma32(join8<T>(lo, hi), pd, dq[dt]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+
+  if (!qvalid) return;
+  const float mul = nan_head ? __builtin_nanf("") : p.scale;
+  const int64_t orow = p.q_rows ? p.q_rows[g] : qrow0 + g;
+  uint8_t* ob = reinterpret_cast<uint8_t*>(p.dq) + 2 * (b * p.dqs[0] + h * p.dqs[1] + orow * p.dqs[2]);
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * half;
+      u32x2 w;
+      w[0] = pack2<T>(dq[dt][4 * g4 + 0] * mul, dq[dt][4 * g4 + 1] * mul);
+      w[1] = pack2<T>(dq[dt][4 * g4 + 2] * mul, dq[dt][4 * g4 + 3] * mul);
+      *reinterpret_cast<u32x2*>(ob + d * 2) = w;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+template <class T>
+static int launch_prep(const PrepParams& pp, hipStream_t s) {
+  const int64_t threads = (int64_t)pp.B * pp.H * pp.ntile * 64 * (pp.D / 8);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipLaunchKernelGGL(bwd_prep_kernel<T>, grid, dim3(256), 0, s, pp);
+  return check_launch("bwd_prep_kernel");
+}
+
+template <int D, class T>
+static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
+  const int BH = p.B * p.H;
+  if (pool && p.dkp) {
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true>), dim3(p.nbkp * BH), dim3(bwd::kThreads), 0, s, p);
+    if (int rc = check_launch("bwd_dkdv_kernel<pooled>")) return rc;
+  }
+  if (p.k) {
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, false>), dim3(p.nbk * BH), dim3(bwd::kThreads), 0, s, p);
+    if (int rc = check_launch("bwd_dkdv_kernel")) return rc;
+  }
+  if (pool)
+    hipLaunchKernelGGL((bwd_dq_kernel<D, T, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
+  else
+    hipLaunchKernelGGL((bwd_dq_kernel<D, T, false>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
+  return check_launch("bwd_dq_kernel");
+}
+
+static int dispatch_bwd(const PrepParams& pp, const BwdParams& p, int D, int dtype, bool pool, hipStream_t s) {
+  if (dtype == VB_DTYPE_BF16) {
+    if (int rc = launch_prep<BF16>(pp, s)) return rc;
+    if (D == 64) return launch_grads<64, BF16>(p, pool, s);
+    return launch_grads<128, BF16>(p, pool, s);
+  }
+  if (int rc = launch_prep<F16>(pp, s)) return rc;
+  if (D == 64) return launch_grads<64, F16>(p, pool, s);
+  return launch_grads<128, F16>(p, pool, s);
+}
+
+struct WsLayout {
+  uint64_t stats, q_r, do_r, dkp, dvp, total;
+};
+static WsLayout ws_layout(int B, int H, int Lq, int D, bool copies, int Lkp) {
+  auto up = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  WsLayout w{};
+  const uint64_t ntile = (uint64_t)((Lq + 63) / 64);
+  uint64_t off = 0;
+  w.stats = off; off = up(off + (uint64_t)B * H * ntile * 256 * 4);
+  w.q_r = w.do_r = 0;
+  if (copies) {
+    w.q_r = off; off = up(off + (uint64_t)B * H * Lq * D * 2);
+    w.do_r = off; off = up(off + (uint64_t)B * H * Lq * D * 2);
+  }
+  w.dkp = w.dvp = 0;
+  if (Lkp > 0) {
+    w.dkp = off; off = up(off + (uint64_t)B * H * Lkp * D * 4);
+    w.dvp = off; off = up(off + (uint64_t)B * H * Lkp * D * 4);
+  }
+  w.total = off;
+  return w;
+}
+
+static bool mul8(const int64_t* s) { return ((s[0] | s[1] | s[2]) & 7) == 0; }
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace vb
+
+extern "C" uint64_t vb_attn_bwd_workspace_size(const vb_attn_bwd_args* a) {
+  if (!a) return 0;
+  return vb::ws_layout(a->B, a->H, a->Lq, a->D, a->q_rows != nullptr, a->kp ? a->Lkp : 0).total;
+}
+
+extern "C" int vb_attn_bwd(const vb_attn_bwd_args* a, void* stream) {
+  using namespace vb;
+  if (!a) return fail(VB_ERR_INVALID, "vb_attn_bwd: null args");
+  if (a->B <= 0 || a->H <= 0 || a->Lq <= 0 || a->Lk <= 0 || a->D <= 0)
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: B, H, Lq, Lk, D must be positive");
+  if (a->D != 64 && a->D != 128)
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_bwd: head_dim must be 64 or 128, got " + std::to_string(a->D));
+  if (a->dtype != VB_DTYPE_BF16 && a->dtype != VB_DTYPE_F16) return fail(VB_ERR_INVALID, "vb_attn_bwd: unknown dtype");
+  if (!a->q || !a->k || !a->v || !a->out || !a->lse || !a->dout || !a->dq || !a->dk || !a->dv)
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: missing tensor");
+  const bool pool = a->kp != nullptr;
+  if (pool && (!a->vp || a->Lkp <= 0 || !a->out2 || !a->lse2 || a->pool_gap <= 0))
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: pooled branch needs vp, Lkp, out2, lse2 and pool_gap");
+  if (pool && (int64_t)a->Lkp * a->pool_gap < a->Lk)
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: Lkp * pool_gap must cover Lk");
+  const int nbk = (a->Lk + 127) / 128;
+  const int nbq = (a->Lq + 127) / 128;
+  if (nbk > bwd::kMaxBlocks || nbq > bwd::kMaxBlocks) return fail(VB_ERR_UNSUPPORTED, "vb_attn_bwd: sequence too long");
+  const int64_t* strides[] = {a->q_stride, a->k_stride, a->v_stride, a->out_stride, a->dout_stride,
+                              a->dq_stride, a->dk_stride, a->dv_stride};
+  for (const int64_t* s : strides)
+    if (!mul8(s)) return fail(VB_ERR_INVALID, "vb_attn_bwd: strides must be multiples of 8 elements");
+  if (pool && (!mul8(a->kp_stride) || !mul8(a->vp_stride) || !mul8(a->out2_stride)))
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: strides must be multiples of 8 elements");
+  const void* ptrs[] = {a->q, a->k, a->v, a->out, a->dout, a->dq, a->dk, a->dv};
+  for (const void* q : ptrs)
+    if (!al16(q)) return fail(VB_ERR_INVALID, "vb_attn_bwd: tensors must be 16-byte aligned");
+  if (pool && (!al16(a->kp) || !al16(a->vp) || !al16(a->out2)))
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: tensors must be 16-byte aligned");
+  const WsLayout w = ws_layout(a->B, a->H, a->Lq, a->D, a->q_rows != nullptr, pool ? a->Lkp : 0);
+  if (!a->workspace || a->workspace_bytes < w.total || !al16(a->workspace))
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: workspace missing or smaller than vb_attn_bwd_workspace_size()");
+  uint8_t* ws = reinterpret_cast<uint8_t*>(a->workspace);
+
+  PrepParams pp{};
+  pp.q = a->q; pp.dout = a->dout; pp.out = a->out; pp.out2 = pool ? a->out2 : nullptr;
+  for (int i = 0; i < 3; ++i) {
+    pp.qs[i] = a->q_stride[i]; pp.dos[i] = a->dout_stride[i]; pp.os[i] = a->out_stride[i];
+    pp.o2s[i] = pool ? a->out2_stride[i] : 0;
+  }
+  pp.lse = a->lse; pp.lse2 = pool ? a->lse2 : nullptr; pp.alpha = a->alpha;
+  pp.q_rows = a->q_rows;
+  pp.stats = reinterpret_cast<float*>(ws + w.stats);
+  if (a->q_rows) { pp.q_r = ws + w.q_r; pp.do_r = ws + w.do_r; }
+  pp.B = a->B; pp.H = a->H; pp.Lq = a->Lq; pp.D = a->D; pp.ntile = (a->Lq + 63) / 64;
+
+  BwdParams p{};
+  if (a->q_rows) {
+    p.q = ws + w.q_r; p.dout = ws + w.do_r;
+    p.qs[0] = p.dos[0] = (int64_t)a->H * a->Lq * a->D;
+    p.qs[1] = p.dos[1] = (int64_t)a->Lq * a->D;
+    p.qs[2] = p.dos[2] = a->D;
+  } else {
+    p.q = a->q; p.dout = a->dout;
+    for (int i = 0; i < 3; ++i) { p.qs[i] = a->q_stride[i]; p.dos[i] = a->dout_stride[i]; }
+  }
+  p.k = a->k; p.v = a->v;
+  for (int i = 0; i < 3; ++i) {
+    p.ks[i] = a->k_stride[i]; p.vs[i] = a->v_stride[i];
+    p.ms[i] = a->mask_stride[i];
+    p.dqs[i] = a->dq_stride[i]; p.dks[i] = a->dk_stride[i]; p.dvs[i] = a->dv_stride[i];
+    if (pool) { p.kps[i] = a->kp_stride[i]; p.vps[i] = a->vp_stride[i]; }
+  }
+  p.kp = pool ? a->kp : nullptr; p.vp = pool ? a->vp : nullptr; p.Lkp = pool ? a->Lkp : 0;
+  p.mask = a->block_mask;
+  p.stats = pp.stats; p.ntile = pp.ntile;
+  p.dq = a->dq; p.q_rows = a->q_rows;
+  p.dk = a->dk; p.dv = a->dv; p.kv_rows = a->kv_rows;
+  if (pool) { p.dkp = reinterpret_cast<float*>(ws + w.dkp); p.dvp = reinterpret_cast<float*>(ws + w.dvp); }
+  p.gap = pool ? a->pool_gap : 1;
+  p.B = a->B; p.H = a->H; p.Lq = a->Lq; p.Lk = a->Lk; p.nbq = nbq; p.nbk = nbk;
+  p.nbkp = pool ? (a->Lkp + 127) / 128 : 0;
+  p.scale = a->scale > 0.f ? a->scale : (float)(1.0 / sqrt((double)a->D));
+  p.c = p.scale * kLog2e;
+  p.heavy_rows = a->heavy_rows;
+  return dispatch_bwd(pp, p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" uint64_t vb_block_sparse_attn_bwd_workspace_size(int batch, int num_heads, int max_seqlen_q) {
+  if (batch <= 0 || num_heads <= 0 || max_seqlen_q <= 0) return 0;
+  return vb::ws_layout(batch, num_heads, max_seqlen_q, 64, false, 0).total;
+}
+
+extern "C" int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, const void* k_unpad,
+                                        const void* v_unpad, const void* out_unpad, const float* softmax_lse,
+                                        const int32_t* cu_seqlens_q, const int32_t* cu_seqlens_k,
+                                        const int32_t* head_mask_type, const int32_t* streaming_info,
+                                        const uint8_t* base_blockmask, int batch, int num_heads, int head_dim,
+                                        int max_seqlen_q, int max_seqlen_k, float p_dropout, float softmax_scale,
+                                        int is_causal, int exact_streaming, int deterministic, int dtype,
+                                        void* dq, void* dk, void* dv, void* workspace, uint64_t workspace_bytes,
+                                        void* stream) {
+  using namespace vb;
+  (void)streaming_info;
+  (void)deterministic;  // always deterministic (no atomics)
+  if (p_dropout != 0.f) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: p_dropout must be 0");
+  if (is_causal || exact_streaming) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: causal/streaming not supported");
+  if (!dout || !q_unpad || !k_unpad || !v_unpad || !out_unpad || !softmax_lse || !cu_seqlens_q || !cu_seqlens_k ||
+      !dq || !dk || !dv)
+    return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: null tensor");
+  if (batch <= 0 || num_heads <= 0 || max_seqlen_q <= 0 || max_seqlen_k <= 0)
+    return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: bad sizes");
+  if (head_dim != 64 && head_dim != 128)
+    return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: head_dim must be 64 or 128");
+  if (dtype != VB_DTYPE_BF16 && dtype != VB_DTYPE_F16) return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: unknown dtype");
+  const int nbq = (max_seqlen_q + 127) / 128;
+  const int nbk = (max_seqlen_k + 127) / 128;
+  if (nbk > bwd::kMaxBlocks || nbq > bwd::kMaxBlocks) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: sequence too long");
+  const WsLayout w = ws_layout(batch, num_heads, max_seqlen_q, head_dim, false, 0);
+  if (!workspace || workspace_bytes < w.total || !al16(workspace))
+    return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: workspace missing or too small");
+  const void* ptrs[] = {dout, q_unpad, k_unpad, v_unpad, out_unpad, dq, dk, dv};
+  for (const void* q : ptrs)
+    if (!al16(q)) return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: tensors must be 16-byte aligned");
+  const int64_t row = (int64_t)num_heads * head_dim;
+  int64_t s3[3] = {0, head_dim, row};
+
+  PrepParams pp{};
+  pp.q = q_unpad; pp.dout = dout; pp.out = out_unpad;
+  for (int i = 0; i < 3; ++i) pp.qs[i] = pp.dos[i] = pp.os[i] = s3[i];
+  pp.lse = softmax_lse;
+  pp.cu_q = cu_seqlens_q;
+  pp.stats = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(workspace) + w.stats);
+  pp.B = batch; pp.H = num_heads; pp.Lq = max_seqlen_q; pp.D = head_dim; pp.ntile = (max_seqlen_q + 63) / 64;
+
+  BwdParams p{};
+  p.q = q_unpad; p.dout = dout; p.k = k_unpad; p.v = v_unpad;
+  for (int i = 0; i < 3; ++i) p.qs[i] = p.dos[i] = p.ks[i] = p.vs[i] = p.dqs[i] = p.dks[i] = p.dvs[i] = s3[i];
+  p.cu_q = cu_seqlens_q; p.cu_k = cu_seqlens_k; p.head_mask_type = head_mask_type;
+  p.mask = base_blockmask;
+  p.ms[0] = head_mask_type ? -1 : (int64_t)num_heads * nbq * nbk;
+  p.ms[1] = (int64_t)nbq * nbk; p.ms[2] = nbk;
+  p.stats = pp.stats; p.ntile = pp.ntile;
+  p.dq = dq; p.dk = dk; p.dv = dv;
+  p.gap = 1;
+  p.B = batch; p.H = num_heads; p.Lq = max_seqlen_q; p.Lk = max_seqlen_k; p.nbq = nbq; p.nbk = nbk;
+  p.scale = softmax_scale > 0.f ? softmax_scale : (float)(1.0 / sqrt((double)head_dim));
+  p.c = p.scale * kLog2e;
+  return dispatch_bwd(pp, p, head_dim, dtype, false, reinterpret_cast<hipStream_t>(stream));
+}

@@ -21,7 +21,7 @@
 // q_rows, so the reference's index_select + cat + reverse (:141-161) cost no pass of their own.
 #include <cstdlib>
 
-#include "vb_common.hpp"
+#include "vb_tiles.hpp"
 
 namespace vb {
 
@@ -74,41 +74,6 @@ __device__ __forceinline__ int v_off_bytes(int row, int col) {
   return row * kRowBytes + 64 * (g ^ sw) + (col & 31) * 2;
 }
 
-template <class T>
-__device__ __forceinline__ typename T::vec8 lds_b128(const uint8_t* base, int off) {
-  return *reinterpret_cast<const typename T::vec8*>(base + off);
-}
-
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-// ds_read_b64_tr_b16 issued from inline asm: hipcc's waitcnt pass treats the builtin form as
-// possibly aliasing the in-flight LDS-DMA writes and drains the whole DMA ring (vmcnt(0)) before
-// it. The asm form is invisible to that pass, so its result must be waited for explicitly with
-// vwait_tr() (a lgkmcnt(0) that names the destinations) before any use.
-__device__ __forceinline__ s16x4 lds_tr4(const uint8_t* base, int off) {
-  const uint32_t a = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)(base + off)));
-  s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-
-template <class T>
-__device__ __forceinline__ typename T::vec8 join8(s16x4 a, s16x4 b) {
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_bit_cast(typename T::vec8, r);
-}
-
-template <class T>
-__device__ __forceinline__ typename T::vec8 pack8(const f32x16& acc, int base) {
-  u32x4 u;
-  u[0] = pack2<T>(acc[base + 0], acc[base + 1]);
-  u[1] = pack2<T>(acc[base + 2], acc[base + 3]);
-  u[2] = pack2<T>(acc[base + 4], acc[base + 5]);
-  u[3] = pack2<T>(acc[base + 6], acc[base + 7]);
-  return __builtin_bit_cast(typename T::vec8, u);
-}
-
 #if VB_DIAG
 // diagnostic-only cycle stamps (never in the product build): per-segment sums of s_memtime
 __device__ unsigned long long g_vb_stamp[16];
@@ -125,9 +90,6 @@ __device__ __forceinline__ unsigned long long vb_stamp() {
 #define VB_STAMP(var)
 #define VB_ACC(i, d)
 #endif
-
-// s_waitcnt vmcnt(n) with lgkm/exp counters left at max (gfx9 encoding)
-#define VB_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
 
 // Describes where tile t's keys come from.
 struct TileSrc {
@@ -173,11 +135,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     bh = blockIdx.x % BH;
   } else {
     const int rows_left = p.nbq - hr;
-    const int id = blockIdx.x - n_heavy;
-    const int nwg = rows_left * BH;
-    const int xcd = id & 7, slot = id >> 3;
-    const int q8 = nwg >> 3, r8 = nwg & 7;
-    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+    const int lin = xcd_linear(blockIdx.x - n_heavy, rows_left * BH);
     bh = lin / rows_left;
     qblk = rows_left - 1 - lin % rows_left;
   }
@@ -197,29 +155,14 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
 
   // ---- which key blocks this q-block keeps ------------------------------------------------------
   const uint8_t* mrow = nullptr;
-  bool dense = (p.mask == nullptr);
+  bool dense = true;
   bool nan_head = false;
-  if (p.use_main && !dense) {
-    int mh = h;
-    if (p.head_mask_type) {
-      const int t = p.head_mask_type[h];
-      if (t == 0) dense = true;
-      else if (t < 0) nan_head = true;
-      else if (t == 1) {
-        int cnt = 0;
-        for (int i = 0; i <= h; ++i) cnt += (p.head_mask_type[i] == 1);
-        mh = cnt - 1;
-      } else {
-        mh = t - 1;
-      }
+  if (p.use_main) {
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
+    if (mh) {
+      dense = false;
+      mrow = mh + (int64_t)qblk * p.ms[2];
     }
-    int64_t mb = p.ms[0];
-    if (mb < 0) {  // reference API: batch stride = (#heads with mask id 1) * nbq * nbk
-      int ones = 0;
-      for (int i = 0; i < p.H; ++i) ones += (p.head_mask_type[i] == 1);
-      mb = (int64_t)ones * p.ms[1];
-    }
-    mrow = p.mask + b * mb + (int64_t)mh * p.ms[1] + (int64_t)qblk * p.ms[2];
   }
   if (threadIdx.x < 64) {
     int n = 0;

@@ -55,6 +55,32 @@ class PredictArgs(ctypes.Structure):
     ]
 
 
+class BwdArgs(ctypes.Structure):
+    """vb_attn_bwd_args (include/vblade.h)."""
+    _fields_ = [
+        ("q", _vp), ("q_stride", _i64x3),
+        ("k", _vp), ("v", _vp), ("k_stride", _i64x3), ("v_stride", _i64x3),
+        ("q_rows", _vp), ("kv_rows", _vp),
+        ("block_mask", _vp), ("mask_stride", _i64x3),
+        ("out", _vp), ("out_stride", _i64x3),
+        ("lse", _vp),
+        ("kp", _vp), ("vp", _vp), ("kp_stride", _i64x3), ("vp_stride", _i64x3),
+        ("Lkp", ctypes.c_int),
+        ("out2", _vp), ("out2_stride", _i64x3),
+        ("lse2", _vp), ("alpha", _vp),
+        ("pool_gap", ctypes.c_int),
+        ("dout", _vp), ("dout_stride", _i64x3),
+        ("dq", _vp), ("dq_stride", _i64x3),
+        ("dk", _vp), ("dv", _vp), ("dk_stride", _i64x3), ("dv_stride", _i64x3),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_uint64),
+        ("B", ctypes.c_int), ("H", ctypes.c_int), ("Lq", ctypes.c_int), ("Lk", ctypes.c_int),
+        ("D", ctypes.c_int),
+        ("scale", ctypes.c_float),
+        ("dtype", ctypes.c_int),
+        ("heavy_rows", ctypes.c_int),
+    ]
+
+
 # name -> (restype, argtypes); must list every symbol include/vblade.h declares
 SIGNATURES = {
     "vb_last_error": (ctypes.c_char_p, []),
@@ -73,6 +99,14 @@ SIGNATURES = {
     "vb_pool_kv": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
+    "vb_attn_bwd_workspace_size": (ctypes.c_uint64, [ctypes.POINTER(BwdArgs)]),
+    "vb_attn_bwd": (ctypes.c_int, [ctypes.POINTER(BwdArgs), _vp]),
+    "vb_block_sparse_attn_bwd_workspace_size": (ctypes.c_uint64, [ctypes.c_int] * 3),
+    "vb_block_sparse_attn_bwd": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
     "vb_lse_combine": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_float, ctypes.c_int, _vp, _vp, _vp]),

@@ -61,16 +61,16 @@ class _AdaptiveSplitFn(torch.autograd.Function):
         out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
                                        need_lse=True)
         out, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
-        ctx.save_for_backward(q, k, v, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp)
+        ctx.save_for_backward(q, k_r, v_r, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp)
         ctx.gap = gap
         return out
 
     @staticmethod
     def backward(ctx, dout):
         from . import backward as bw
-        q, k, v, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp = ctx.saved_tensors
-        dq, dk, dv = bw.adaptive_split_bwd(dout, q, k, v, mask, rows, out1, lse1, out2, lse2,
-                                           alpha, kp, vp, ctx.gap)
+        q, k_r, v_r, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp = ctx.saved_tensors
+        dq, dk, dv = bw.adaptive_split_bwd(dout.contiguous(), q, k_r, v_r, mask, rows, out1, lse1,
+                                           out2, lse2, alpha, kp, vp, ctx.gap, heavy_rows=2)
         return dq, dk, dv, None, None, None
 
 

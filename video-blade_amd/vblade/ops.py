@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import AttnArgs, PredictArgs, check
+from ._lib import AttnArgs, BwdArgs, PredictArgs, check
 
 BLOCK = 128
 
@@ -171,6 +171,111 @@ def block_sparse_attn_fwd(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k,
         int(bool(exact_streaming)), _dtype_code(q_unpad), out.data_ptr(), lse.data_ptr(),
         _stream(dev)), "vb_block_sparse_attn_fwd")
     return out, lse
+
+
+# ----------------------------------------------------------------------------------------------
+# backward
+# ----------------------------------------------------------------------------------------------
+def _mask_u8(block_mask, Lq, Lk):
+    if block_mask is None:
+        return None
+    if block_mask.dtype == torch.bool:
+        block_mask = block_mask.view(torch.uint8)
+    nbq, nbk = (Lq + BLOCK - 1) // BLOCK, (Lk + BLOCK - 1) // BLOCK
+    if block_mask.shape[2] < nbq or block_mask.shape[3] < nbk:
+        raise ValueError(f"block_mask {tuple(block_mask.shape)} too small for {nbq}x{nbk} blocks")
+    if block_mask.stride(3) != 1:
+        block_mask = block_mask.contiguous()
+    return block_mask
+
+
+def attention_bwd(dout, q, k, v, out, lse, *, block_mask=None, q_rows=None, kv_rows=None,
+                  kp=None, vp=None, out2=None, lse2=None, alpha=None, gap: int = 0,
+                  scale: Optional[float] = None, heavy_rows: int = 0, dk_rows: Optional[int] = None):
+    """vb_attn_bwd: gradients (dq, dk, dv) of the block-sparse attention, optionally of the
+    adaptive two-branch form (kp/vp/out2/lse2/alpha/gap: alpha detached, pooled grads folded back
+    through the mean pool). k/v hold keys in reordered order; dk/dv rows are written at
+    kv_rows[g] (dk_rows = number of rows of dk/dv, default Lk). Returns bf16/fp16 tensors."""
+    dev = _require_gpu(dout, q, k, v, out, lse, block_mask, q_rows, kv_rows, kp, vp, out2, lse2,
+                       alpha)
+    q, k, v, out, dout = (_aligned_bhld(t) for t in (q, k, v, out, dout))
+    B, H, Lq, D = q.shape
+    Lk = k.shape[2]
+    nrows = Lk if dk_rows is None else int(dk_rows)
+    dq = torch.empty(B, H, Lq, D, device=dev, dtype=q.dtype)
+    dk = torch.empty(B, H, nrows, D, device=dev, dtype=q.dtype)
+    dv = torch.empty(B, H, nrows, D, device=dev, dtype=q.dtype)
+    a = BwdArgs()
+    a.q, a.q_stride = q.data_ptr(), _s3(q)
+    a.k, a.v, a.k_stride, a.v_stride = k.data_ptr(), v.data_ptr(), _s3(k), _s3(v)
+    a.q_rows, a.kv_rows = _ptr(q_rows), _ptr(kv_rows)
+    m = _mask_u8(block_mask, Lq, Lk)
+    if m is not None:
+        a.block_mask = m.data_ptr()
+        a.mask_stride = (ctypes.c_int64 * 3)(m.stride(0), m.stride(1), m.stride(2))
+    a.out, a.out_stride = out.data_ptr(), _s3(out)
+    lse = lse.float().contiguous()
+    a.lse = lse.data_ptr()
+    if kp is not None:
+        kp, vp, out2 = _aligned_bhld(kp), _aligned_bhld(vp), _aligned_bhld(out2)
+        lse2 = lse2.float().contiguous()
+        alpha = alpha.float().contiguous()
+        a.kp, a.vp, a.kp_stride, a.vp_stride = kp.data_ptr(), vp.data_ptr(), _s3(kp), _s3(vp)
+        a.Lkp = kp.shape[2]
+        a.out2, a.out2_stride = out2.data_ptr(), _s3(out2)
+        a.lse2, a.alpha = lse2.data_ptr(), alpha.data_ptr()
+        a.pool_gap = int(gap)
+    a.dout, a.dout_stride = dout.data_ptr(), _s3(dout)
+    a.dq, a.dq_stride = dq.data_ptr(), _s3(dq)
+    a.dk, a.dv, a.dk_stride, a.dv_stride = dk.data_ptr(), dv.data_ptr(), _s3(dk), _s3(dv)
+    a.B, a.H, a.Lq, a.Lk, a.D = B, H, Lq, Lk, D
+    a.scale = float(scale) if scale else 0.0
+    a.dtype = _dtype_code(q)
+    a.heavy_rows = int(heavy_rows)
+    lib = _lib.load()
+    nbytes = int(lib.vb_attn_bwd_workspace_size(ctypes.byref(a)))
+    ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
+    check(lib.vb_attn_bwd(ctypes.byref(a), _stream(dev)), "vb_attn_bwd")
+    return dq, dk, dv
+
+
+def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_lse, cu_seqlens_q,
+                          cu_seqlens_k, head_mask_type, streaming_info, base_blockmask,
+                          max_seqlen_q, max_seqlen_k, p_dropout=0.0, softmax_scale=None,
+                          is_causal=False, exact_streaming=False, deterministic=True):
+    """Backward of block_sparse_attn_func (vb_block_sparse_attn_bwd, varlen layout).
+    Returns (dq, dk, dv) [total, H, D]."""
+    dev = _require_gpu(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_lse, base_blockmask)
+    dout, q_unpad, k_unpad, v_unpad, out_unpad = (t.contiguous() for t in
+                                                  (dout, q_unpad, k_unpad, v_unpad, out_unpad))
+    B = cu_seqlens_q.numel() - 1
+    H, D = q_unpad.shape[1], q_unpad.shape[2]
+    nbq = (max_seqlen_q + BLOCK - 1) // BLOCK
+    nbk = (max_seqlen_k + BLOCK - 1) // BLOCK
+    mask = None
+    if base_blockmask is not None:
+        mask = base_blockmask[:, :, :nbq, :nbk]
+        if mask.dtype == torch.bool:
+            mask = mask.contiguous().view(torch.uint8)
+        mask = mask.to(torch.uint8).contiguous()
+    hmt = head_mask_type.to(device=dev, dtype=torch.int32).contiguous() if head_mask_type is not None else None
+    cu_q = cu_seqlens_q.to(torch.int32).contiguous()
+    cu_k = cu_seqlens_k.to(torch.int32).contiguous()
+    lse = softmax_lse.float().contiguous()
+    dq, dk, dv = torch.empty_like(q_unpad), torch.empty_like(k_unpad), torch.empty_like(v_unpad)
+    lib = _lib.load()
+    nbytes = int(lib.vb_block_sparse_attn_bwd_workspace_size(B, H, int(max_seqlen_q)))
+    ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
+    check(lib.vb_block_sparse_attn_bwd(
+        dout.data_ptr(), q_unpad.data_ptr(), k_unpad.data_ptr(), v_unpad.data_ptr(),
+        out_unpad.data_ptr(), lse.data_ptr(), cu_q.data_ptr(), cu_k.data_ptr(), _ptr(hmt),
+        _ptr(streaming_info), _ptr(mask), B, H, D, int(max_seqlen_q), int(max_seqlen_k),
+        float(p_dropout), float(softmax_scale) if softmax_scale else 0.0, int(bool(is_causal)),
+        int(bool(exact_streaming)), int(bool(deterministic)), _dtype_code(q_unpad),
+        dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(), nbytes, _stream(dev)),
+        "vb_block_sparse_attn_bwd")
+    return dq, dk, dv
 
 
 # ----------------------------------------------------------------------------------------------
