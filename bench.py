@@ -20,10 +20,15 @@ over ranks, value = all ranks' frames / time ("scaling": "weak").
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import math
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import torch
@@ -53,6 +58,8 @@ def parse():
     ap.add_argument("--sets", type=int, default=3, help="distinct resident q/k/v sets")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes (roofline.traffic = null)")
     return ap.parse_args()
 
 
@@ -78,6 +85,24 @@ def attn_flops(mask: torch.Tensor, L: int, D: int, Lkp: int) -> float:
     return 4.0 * D * pairs + 4.0 * heads * L * Lkp * D
 
 
+def max_over_ranks(elapsed: float, dev) -> float:
+    """The job's time = the slowest rank's (weak scaling: every rank renders its own videos).
+    Works on any initialised process group (RCCL on the GPU box, gloo in the CPU tests)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed
+    if dist.get_backend() != "nccl":
+        dev = torch.device("cpu")
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def whole_job_frames_per_s(world: int, frames: int, steps: int, elapsed: float) -> float:
+    """value = frames rendered by ALL ranks / the job's time."""
+    return world * frames * steps / elapsed
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,7 +116,6 @@ def main():
     torch.cuda.set_device(dev)
 
     import vblade
-    from vblade import ops
 
     V = VARIANTS[args.variant]
     H, D, layers, frames = V["H"], V["D"], V["layers"], V["frames"]
@@ -116,6 +140,11 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
+        # the dominant kernel is timed live: HIP events around every attention launch, recorded
+        # on the launch stream inside the timed region (rank 0; two event records per call)
+        rng_state = torch.cuda.get_rng_state(dev)
+        if rank == 0:
+            mod.attn_events = []
         t0 = time.perf_counter()
         for _ in range(args.steps):
             one_video()
@@ -124,13 +153,11 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
+        events, mod.attn_events = mod.attn_events, None
+    elapsed = max_over_ranks(elapsed, dev)
     ms_per_step = 1000.0 * elapsed / args.steps
     ms_per_call = ms_per_step / calls
-    value = world * frames * args.steps / elapsed
+    value = whole_job_frames_per_s(world, frames, args.steps, elapsed)
     sparsity = mod.sparsity
 
     result = {
@@ -165,7 +192,7 @@ def main():
 
     if rank == 0:
         with torch.no_grad():
-            extra = measure_kernels(mod, sets, L, H, D, dev, ops, args)
+            extra = measure_kernels(mod, sets, L, H, D, dev, args, events, rng_state, calls)
         result.update(extra["top"])
         dense_ms = extra.get("dense_ms")
         if dense_ms:
@@ -173,6 +200,12 @@ def main():
             result["speedup_vs_dense_sdpa"] = round(dense_ms / ms_per_call, 3)
             dense_flops = 4.0 * H * L * L * D
             result["attn_tflops_dense_equiv"] = round(dense_flops / (ms_per_call * 1e-3) / 1e12, 2)
+        if not args.no_pmc and world == 1:
+            traffic = pmc_traffic(args.variant)
+            if traffic is not None:
+                result["roofline"]["traffic"] = traffic["bytes"]
+                result["roofline"]["traffic_detail"] = traffic
+        result["roofline"]["algorithmic_bytes"] = extra["alg_bytes"]
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args.variant, calls, frames)
         print(json.dumps(result), flush=True)
@@ -181,40 +214,26 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def measure_kernels(mod, sets, L, H, D, dev, ops, args):
-    """Average duration of the dominant kernel (attn_fwd_kernel) with HIP events on the stream
-    it runs on, its algorithmic FLOPs, and dense SDPA on the same shapes for the ratio."""
-    stream = torch.cuda.current_stream(dev)
-    rows = mod._rows(dev)
-    recs = []
-    for s, (q, k, v) in enumerate(sets):
-        _, mask = mod.predict_mask(q, k)
-        kp, vp, k_r, v_r = ops.pool_kv(k, v, mod.sample_gap, rows, reordered=True)
-        recs.append((q, k_r, v_r, mask, kp, vp))
-    n_rep = 10
+def measure_kernels(mod, sets, L, H, D, dev, args, events, rng_state, calls):
+    """Roofline of the dominant kernel (attn_fwd_kernel): its average launch duration from the
+    HIP events recorded around every launch of the timed region, and its algorithmic FLOPs
+    recomputed exactly per launch by replaying the timed region's mask predictions (same RNG
+    state, same inputs -> the same sampled offsets and masks; no attention run). Plus dense
+    SDPA on the same shapes for the speedup ratio."""
+    ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
+    torch.cuda.set_rng_state(rng_state, dev)
     flops = 0.0
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(n_rep * len(recs))]
-    i = 0
-    for _ in range(2):   # warm
-        for q, k, v, mask, kp, vp in recs:
-            ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
-                              kp_log_bias=math.log(mod.sample_gap), heavy_rows=mod.force_tail)
-    for _ in range(n_rep):
-        for q, k, v, mask, kp, vp in recs:
-            a, b = ev[i]
-            a.record(stream)
-            ops.attention_fwd(q, k, v, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
-                              kp_log_bias=math.log(mod.sample_gap), heavy_rows=mod.force_tail)
-            b.record(stream)
-            flops += attn_flops(mask, L, D, kp.shape[2])
-            i += 1
-    torch.cuda.synchronize()
-    ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-    flops /= len(ev)
+    Lkp = (L + mod.sample_gap - 1) // mod.sample_gap
+    n = 0
+    for _ in range(args.steps):
+        for c in range(calls):
+            q, k, _ = sets[c % len(sets)]
+            _, mask = mod.predict_mask(q, k)
+            flops += attn_flops(mask, L, D, Lkp)
+            n += 1
+    assert n == len(events)
+    flops /= n
     achieved = flops / (ms * 1e-3) / 1e12
-    # compulsory HBM bytes of one launch: Q, O once; K/V of kept blocks (upper bound: all of K,V
-    # once), pooled K/V, mask (for the roofline's traffic cross-check)
     top = {
         "roofline": {
             "bound": "mfma",
@@ -225,12 +244,17 @@ def measure_kernels(mod, sets, L, H, D, dev, ops, args):
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
             "traffic": None,
             "avg_launch_ms": round(ms, 4),
+            "launches_timed": n,
             "flops_per_launch": flops,
         }
     }
-    out = {"top": top}
+    # compulsory bytes of one launch: Q read + O written once, every K/V row read at
+    # least once (the kept blocks cover every key block), pooled K/V, the mask
+    alg_bytes = H * (4 * L * D * 2) + H * 2 * Lkp * D * 2 + H * ((L + 127) // 128) ** 2
+    out = {"top": top, "alg_bytes": alg_bytes}
     if not args.no_dense:
         q, k, v = sets[0]
+        stream = torch.cuda.current_stream(dev)
         for _ in range(2):
             torch.nn.functional.scaled_dot_product_attention(q, k, v)
         torch.cuda.synchronize()
@@ -242,6 +266,44 @@ def measure_kernels(mod, sets, L, H, D, dev, ops, args):
         torch.cuda.synchronize()
         out["dense_ms"] = a.elapsed_time(b) / 5
     return out
+
+
+def pmc_traffic(variant, timeout=300):
+    """HBM-side bytes per attn_fwd_kernel launch from rocprofv3 PMC counters, one counter per
+    pass (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
+    tallies wide coalesced reads at half their bytes, so traffic = 2*FETCH + WRITE. The target
+    is tools/attn_only.py: the same kernel on the same shapes, in a child process."""
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None
+    vals = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="vb_pmc_", dir="/tmp")
+        cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.join(ROOT, "tools", "attn_only.py"), variant, "3", "attn"]
+        try:
+            subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, check=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except (subprocess.SubprocessError, OSError):
+            shutil.rmtree(d, ignore_errors=True)
+            return None
+        xs = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if "attn_fwd_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                    xs.append(float(r["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not xs:
+            return None
+        vals[counter] = sum(xs) / len(xs)
+    read_b = 2.0 * vals["FETCH_SIZE"] * 1024.0
+    write_b = vals["WRITE_SIZE"] * 1024.0
+    return {"bytes": round(read_b + write_b), "read_bytes": round(read_b),
+            "write_bytes": round(write_b), "FETCH_SIZE_KiB": vals["FETCH_SIZE"],
+            "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
+            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on tools/attn_only.py; "
+                      "traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)"}
 
 
 def cpu_baseline(variant, calls, frames):

@@ -31,7 +31,7 @@ with torch.no_grad():
     for _ in range(n):
         if what in ("attn", "all"):
             ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
-                              kp_log_bias=math.log(m.sample_gap))
+                              kp_log_bias=math.log(m.sample_gap), heavy_rows=m.force_tail)
         if what in ("pred", "all"):
             m.predict_mask(q, k, qo, ko)
     torch.cuda.synchronize()

@@ -131,6 +131,9 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self._kept_slots = None
         self._slot_totals = []
         self.last_mask: Optional[torch.Tensor] = None
+        # optional list: when set, every fused attention launch is bracketed by a pair of HIP
+        # events on the launch stream (bench.py's live kernel timing); None = no events
+        self.attn_events: Optional[list] = None
 
     # -------------------------------------------------------------------------------- helpers
     def _rows(self, device):
@@ -211,9 +214,17 @@ class AdaptiveBlockSparseAttn(nn.Module):
             # one pass over K/V: pooled K/V + Gilbert-ordered contiguous copies the attention
             # kernel streams by LDS-DMA; q rows gathered and out rows scattered in the kernel
             kp, vp, k_r, v_r = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True)
+            ev = self.attn_events
+            if ev is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             out = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
                                     kp_log_bias=math.log(self.sample_gap),
                                     heavy_rows=self.force_tail)
+            if ev is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                ev.append((e0, e1))
         if self.log_every and self.sparsity_counter % self.log_every == 0:
             print(f"sparsity: {self.sparsity}")
         return out
