@@ -258,19 +258,47 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       my_chunk[i] = (((sl >> 2) ^ vsw) << 2) | (sl & 3);
     }
   }
+  // Buffer descriptors of this wave's matrix for the (b,h) slice (main and pooled keys): the DMA
+  // then needs no 64-bit per-lane address math — the lane's fixed part (row within the tile,
+  // source chunk) is a precomputed 32-bit voffset and the tile's first key a scalar soffset.
+  // The host guarantees every slice spans < 2^31 bytes.
+  const int my_rowb = (int)my_stride;
+  const int my_prowb = (int)my_pstride;
+  const srd_t my_rsrc = make_srd(my_base, p.use_main ? (int)((int64_t)(Lk - 1) * my_stride + kRowB) : 0);
+  const srd_t my_prsrc = make_srd(kPool ? my_pbase : my_base, kPool ? (int)((int64_t)(p.Lkp - 1) * my_pstride + kRowB) : 0);
+  int my_voff[kInstPerWave], my_pvoff[kInstPerWave];
+#pragma unroll
+  for (int i = 0; i < kInstPerWave; ++i) {
+    my_voff[i] = my_row[i] * my_rowb + my_chunk[i] * 16;
+    my_pvoff[i] = my_row[i] * my_prowb + my_chunk[i] * 16;
+  }
   auto issue = [&](int t) __attribute__((always_inline)) {
     const TileSrc src = tile_src(t);
     uint8_t* dst = smem + (t % kBufs) * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
     const bool pooled = kPool && src.pooled;
-    const uint8_t* base = pooled ? my_pbase : my_base;
-    const int64_t stride = pooled ? my_pstride : my_stride;
+    if (kKvRows && !pooled) {   // gathered k/v rows (generic API path; serialises the ring)
 #pragma unroll
-    for (int i = 0; i < kInstPerWave; ++i) {
-      int key = src.kstart + min(my_row[i], src.klen - 1);
-      if (kKvRows && !pooled) key = p.kv_rows[key];  // gathered k/v rows (slower: serialises the ring)
-      const uint8_t* gsrc = base + (int64_t)key * stride + my_chunk[i] * 16;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+      for (int i = 0; i < kInstPerWave; ++i) {
+        int key = src.kstart + min(my_row[i], src.klen - 1);
+        key = p.kv_rows[key];
+        const uint8_t* gsrc = my_base + (int64_t)key * my_stride + my_chunk[i] * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                         (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+      }
+      return;
+    }
+    const int rowb = pooled ? my_prowb : my_rowb;
+    const int soff = __builtin_amdgcn_readfirstlane(src.kstart * rowb);
+    if (src.klen == kKT) {
+#pragma unroll
+      for (int i = 0; i < kInstPerWave; ++i)
+        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, pooled ? my_pvoff[i] : my_voff[i], soff);
+    } else {   // tail tile: clamp rows to the last valid key (replicated rows are masked later)
+#pragma unroll
+      for (int i = 0; i < kInstPerWave; ++i) {
+        const int r = min(my_row[i], src.klen - 1);
+        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, r * rowb + my_chunk[i] * 16, soff);
+      }
     }
   };
 
@@ -509,6 +537,11 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
     if (a->use_main && ((a->k_stride[i] | a->v_stride[i]) & 7)) return fail(VB_ERR_INVALID, "vb_attn_fwd: k/v strides must be multiples of 8 elements");
     if (pool && ((a->kp_stride[i] | a->vp_stride[i]) & 7)) return fail(VB_ERR_INVALID, "vb_attn_fwd: kp/vp strides must be multiples of 8 elements");
   }
+  const int64_t kLim = int64_t(1) << 31;   // one (b,h) slice must be addressable by a 32-bit buffer offset
+  if (a->use_main && ((int64_t)(a->Lk - 1) * 2 * (a->k_stride[2] > a->v_stride[2] ? a->k_stride[2] : a->v_stride[2]) + 2 * a->D >= kLim))
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: a k/v (b,h) slice spans >= 2 GiB");
+  if (pool && ((int64_t)(a->Lkp - 1) * 2 * (a->kp_stride[2] > a->vp_stride[2] ? a->kp_stride[2] : a->vp_stride[2]) + 2 * a->D >= kLim))
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: a kp/vp (b,h) slice spans >= 2 GiB");
   if (!aligned16(a->q) || !aligned16(a->out) || (a->use_main && (!aligned16(a->k) || !aligned16(a->v))) ||
       (pool && (!aligned16(a->kp) || !aligned16(a->vp))))
     return fail(VB_ERR_INVALID, "vb_attn_fwd: tensors must be 16-byte aligned");
@@ -555,6 +588,8 @@ extern "C" int vb_block_sparse_attn_fwd(const void* q_unpad, const void* k_unpad
   const int nbq = (max_seqlen_q + kQBlk - 1) / kQBlk;
   const int nbk = (max_seqlen_k + kQBlk - 1) / kQBlk;
   if (nbk > kMaxBlocks) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_fwd: max_seqlen_k too long");
+  if ((int64_t)(max_seqlen_k - 1) * 2 * num_heads * head_dim + 2 * head_dim >= (int64_t(1) << 31))
+    return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_fwd: a sequence's k/v span >= 2 GiB");
   FwdParams p{};
   p.q = q_unpad; p.k = k_unpad; p.v = v_unpad;
   const int64_t row = (int64_t)num_heads * head_dim;

@@ -51,6 +51,28 @@ __device__ __forceinline__ typename T::vec8 pack8(const f32x16& acc, int base) {
   return __builtin_bit_cast(typename T::vec8, u);
 }
 
+// ---- LDS-DMA through a buffer descriptor ------------------------------------------------------------
+// (base, extent) of a wave-uniform buffer; the descriptor itself is built inside dma16 (the compiler
+// keeps it in SGPRs and hoists it), so host-side parsing of kernels never sees the device-only
+// resource type. `bytes` < 2^31.
+struct srd_t {
+  const void* base;
+  int bytes;
+};
+__device__ __forceinline__ srd_t make_srd(const void* base, int bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  return srd_t{reinterpret_cast<const void*>((static_cast<uint64_t>(hi) << 32) | lo),
+               __builtin_amdgcn_readfirstlane(bytes)};
+}
+// 16 bytes per lane from base + voffset + soffset into lds + 16 * lane (buffer_load_dwordx4 ... lds)
+__device__ __forceinline__ void dma16(srd_t srd, uint8_t* lds, int voffset, int soffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(srd.base), (short)0, srd.bytes, 0x00020000),
+      (__attribute__((address_space(3))) void*)lds, 16, voffset, soffset, 0, 0);
+}
+
 // ---- dual-use LDS image ---------------------------------------------------------------------------
 // A [rows][D] 16-bit tile read BOTH row-wise (ds_read_b128: 16 lanes = 16 consecutive rows, one
 // 16-byte chunk) and transposed (ds_read_b64_tr_b16: a half-wave = 4 consecutive rows x 64 bytes),
