@@ -20,6 +20,7 @@
 // Gilbert reorder: q/k/v rows are gathered through q_rows / kv_rows and O/LSE scattered through
 // q_rows, so the reference's index_select + cat + reverse (:141-161) cost no pass of their own.
 #include <cstdlib>
+#include <type_traits>
 
 #include "vb_tiles.hpp"
 
@@ -272,9 +273,9 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     my_voff[i] = my_row[i] * my_rowb + my_chunk[i] * 16;
     my_pvoff[i] = my_row[i] * my_prowb + my_chunk[i] * 16;
   }
-  auto issue = [&](int t) __attribute__((always_inline)) {
+  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
     const TileSrc src = tile_src(t);
-    uint8_t* dst = smem + (t % kBufs) * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
+    uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
     const bool pooled = kPool && src.pooled;
     if (kKvRows && !pooled) {   // gathered k/v rows (generic API path; serialises the ring)
 #pragma unroll
@@ -316,14 +317,29 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   unsigned long long acc_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
-  // One 64-key tile: S^T = K.Q^T, online softmax, O^T += V^T.P^T.
-  auto tile_step = [&](const uint8_t* kl, const uint8_t* vl, float bias, int klen) __attribute__((always_inline)) {
+  // Loop-invariant per-lane LDS addresses: the images' XOR swizzles depend only on the lane's own
+  // row bits (K: row l32 [+32 kt]; V: row vrow [+16 k + 8]), so every K/V fragment read of every
+  // tile and ring slot is one of these bases plus a compile-time immediate offset.
+  int k_lane[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) k_lane[ks] = k_off<D>(l32, 2 * ks + half);
+  uint32_t v_lane[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+    v_lane[dt] = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                     (__attribute__((address_space(3))) const uint8_t*)smem)) +
+                 v_off_bytes<D>(vrow, dt * 32 + vcol);
+
+  // One 64-key tile in ring slot U: S^T = K.Q^T, online softmax, O^T += V^T.P^T.
+  auto tile_step = [&](auto U, float bias, int klen) __attribute__((always_inline)) {
+    constexpr int kSlot = decltype(U)::value;
+    const uint8_t* kl = smem + kSlot * kBufBytes;
     f32x16 s[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       typename T::vec8 kf[KS];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(kl, k_off<D>(kt * 32 + l32, 2 * ks + half));
+      for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(kl + kt * 32 * kRowB, k_lane[ks]);
 #pragma unroll
       for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
 #pragma unroll
@@ -334,11 +350,11 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     constexpr int VPRE = (D == 64) ? 4 : 2;
     s16x4 vlo[4][DT], vhi[4][DT];
     auto read_v = [&](int kk) __attribute__((always_inline)) {
-      const int kb = (kk >> 1) * 32 + 16 * (kk & 1) + vrow;
+      const int row0 = (kk >> 1) * 32 + 16 * (kk & 1);   // + vrow (in v_lane)
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        vlo[kk][dt] = lds_tr4(vl, v_off_bytes<D>(kb, dt * 32 + vcol));
-        vhi[kk][dt] = lds_tr4(vl, v_off_bytes<D>(kb + 8, dt * 32 + vcol));
+        vlo[kk][dt] = lds_tr4_imm(v_lane[dt], kSlot * kBufBytes + kMatBytes + row0 * kRowB);
+        vhi[kk][dt] = lds_tr4_imm(v_lane[dt], kSlot * kBufBytes + kMatBytes + (row0 + 8) * kRowB);
       }
     };
     auto wait_v = [&](int kk) __attribute__((always_inline)) {
@@ -360,12 +376,14 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     // row max: four independent chains (short dependency chains, max3-friendly)
     float mq[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) mq[c] = fmaxf(s[c >> 1][8 * (c & 1)], s[c >> 1][8 * (c & 1) + 1]);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int r = 2; r < 8; ++r) mq[c] = fmaxf(mq[c], s[c >> 1][8 * (c & 1) + r]);
-    float mt = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
+    for (int c = 0; c < 4; ++c) {   // 16 v_max3 for 32 values (the minimum), depth 6
+      const f32x16& x = s[c >> 1];
+      const int o = 8 * (c & 1);
+      mq[c] = max3f(max3f(max3f(x[o], x[o + 1], x[o + 2]), x[o + 3], x[o + 4]), x[o + 5], x[o + 6]);
+    }
+    const float f1 = max3f(mq[0], mq[1], s[0][7]);
+    const float f2 = max3f(mq[2], mq[3], s[0][15]);
+    float mt = max3f(max3f(f1, f2, s[1][7]), s[1][15], s[1][15]);
     mt = max_xor32(mt) * p.c + bias;            // tile row max, exp2 domain
     // lazy rescale: only when some row's running max grows (exact; no threshold). The empty
     // volatile asm keeps hipcc from if-converting this rare block into every iteration.
@@ -419,9 +437,12 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     VB_ACC(4, s3 - s2);
   };
 
-  for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
-  for (int t = 0; t < ntiles; ++t) {
-    VB_STAMP(t0);
+  for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t, t);
+  // The loop body is instantiated once per ring slot (compile-time U), so every LDS address is a
+  // loop-invariant lane base + immediate offset: no address VALU inside the loop.
+  auto body = [&](int t, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+    VB_STAMP(st0);
     // retire this wave's DMAs of tile t (younger tiles stay in flight); the barrier then makes
     // every wave's part visible and proves slot (t-1) % kBufs is no longer being read
     const int younger = min(ntiles - 1 - t, kBufs - 2);
@@ -430,18 +451,23 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     else VB_WAIT_VMCNT(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    VB_STAMP(t1);
-    VB_ACC(0, t1 - t0);
-    if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
-    VB_STAMP(t2);
-    VB_ACC(1, t2 - t1);
+    VB_STAMP(st1);
+    VB_ACC(0, st1 - st0);
+    if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1, (u + kBufs - 1) % kBufs);
+    VB_STAMP(st2);
+    VB_ACC(1, st2 - st1);
     const TileSrc src = tile_src(t);
     const float bias = (kPool && src.pooled) ? p.pool_bias_l2 : 0.f;
-    const uint8_t* kl = smem + (t % kBufs) * kBufBytes;
-    if (VB_DIAG && (p.dbg & 2)) continue;   // diagnostic: stream tiles only
-    tile_step(kl, kl + kMatBytes, bias, src.klen);
-    VB_STAMP(t3);
-    VB_ACC(2, t3 - t2);
+    if (VB_DIAG && (p.dbg & 2)) return;   // diagnostic: stream tiles only
+    tile_step(U, bias, src.klen);
+    VB_STAMP(st3);
+    VB_ACC(2, st3 - st2);
+  };
+  for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
+    body(t0, std::integral_constant<int, 0>{});
+    if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
+    if constexpr (kBufs > 2)
+      if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
   }
 #if VB_DIAG
   if (lane == 0) {

@@ -34,6 +34,13 @@ __device__ __forceinline__ s16x4 lds_tr4(const uint8_t* base, int off) {
   return r;
 }
 
+// the same with a compile-time immediate offset on a loop-invariant lane address
+__device__ __forceinline__ s16x4 lds_tr4_imm(uint32_t lane_addr, int imm) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lane_addr), "i"(imm));
+  return r;
+}
+
 template <class T>
 __device__ __forceinline__ typename T::vec8 join8(s16x4 a, s16x4 b) {
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -49,6 +56,14 @@ __device__ __forceinline__ typename T::vec8 pack8(const f32x16& acc, int base) {
   u[2] = pack2<T>(acc[base + 4], acc[base + 5]);
   u[3] = pack2<T>(acc[base + 6], acc[base + 7]);
   return __builtin_bit_cast(typename T::vec8, u);
+}
+
+// max of three floats as ONE v_max3_f32. Through fmaxf hipcc first canonicalises every MFMA
+// result with a v_max x,x (IEEE sNaN quieting): an extra VALU per score on the softmax path.
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
 
 // ---- LDS-DMA through a buffer descriptor ------------------------------------------------------------
