@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""A/B timing of library variants (video-blade_amd/vblade/variants/lib_<tag>.so) in ONE process on
+ONE GPU: the same inputs, launches interleaved A,B,A,B,... so clock/device drift cancels.
+usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred|call]"""
+import argparse
+import ctypes
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
+sys.path.insert(0, ROOT)
+import vblade  # noqa: E402
+from vblade import _lib, ops  # noqa: E402
+from bench import attn_flops, realistic_qkv  # noqa: E402
+
+
+def load(tag):
+    path = os.path.join(ROOT, "video-blade_amd", "vblade", "variants", f"lib_{tag}.so")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _lib.SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tags", nargs="+")
+    ap.add_argument("--variant", default="both")
+    ap.add_argument("--what", default="attn")
+    ap.add_argument("--rounds", type=int, default=15)
+    a = ap.parse_args()
+    libs = {t: load(t) for t in set(a.tags)}
+    keys = [f"{t}#{i}" for i, t in enumerate(a.tags)]
+    dev = torch.device("cuda")
+    for variant in (["cog", "wan"] if a.variant == "both" else [a.variant]):
+        H, D = (48, 64) if variant == "cog" else (12, 128)
+        m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+        L = m.gilbert_rearranger.seq_len
+        q, k, v = realistic_qkv(H, L, D, 0, dev)
+        rows = m._rows(dev)
+        qo = vblade.draw_sample_offsets(1, H, dev)
+        ko = vblade.draw_sample_offsets(1, H, dev)
+        _lib._lib = libs[a.tags[0]]
+        _, mask = m.predict_mask(q, k, qo, ko)
+        kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
+        fl = attn_flops(mask, L, D, kp.shape[2])
+        if a.what == "attn":
+            fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp,  # noqa
+                                           vp=vp, kp_log_bias=math.log(m.sample_gap),
+                                           heavy_rows=m.force_tail)
+        elif a.what == "pred":
+            fn = lambda: m.predict_mask(q, k, qo, ko)  # noqa
+        else:
+            fn = lambda: m(q, k, v)  # noqa
+        ref = None
+        times = {kk: [] for kk in keys}
+        with torch.no_grad():
+            for t in a.tags:   # warm + cross-check outputs (a repeated tag checks determinism)
+                _lib._lib = libs[t]
+                out = fn()
+                torch.cuda.synchronize()
+                if a.what == "attn":
+                    if ref is None:
+                        ref = out.float()
+                    else:
+                        err = (out.float() - ref).abs().max().item()
+                        print(f"  {t}: max|out - {a.tags[0]}| = {err:.3e}")
+            for _ in range(a.rounds):
+                for kk, t in zip(keys, a.tags):
+                    _lib._lib = libs[t]
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(5):
+                        fn()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    times[kk].append(e0.elapsed_time(e1) / 5)
+        base = statistics.median(times[keys[0]])
+        for kk, t in zip(keys, a.tags):
+            md = statistics.median(times[kk])
+            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what == "attn" else ""
+            print(f"{variant} {a.what} {kk}: median {md:.4f} ms (min {min(times[kk]):.4f}){extra}  "
+                  f"x{base / md:.3f} vs {a.tags[0]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build the current sources into video-blade_amd/vblade/variants/lib_<TAG>.so (A/B timing, tools/ab.py)
+set -e
+TAG=${1:?tag}
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+B=/tmp/vb_variant_$TAG
+mkdir -p $B "$ROOT/video-blade_amd/vblade/variants"
+FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$ROOT/include -I$ROOT/video-blade_amd/csrc ${VB_EXTRA_FLAGS}"
+for f in "$ROOT"/video-blade_amd/csrc/*.hip "$ROOT"/video-blade_amd/csrc/*.cpp; do
+  extra=""; case "$f" in *vb_attn_fwd.hip) extra="-fno-slp-vectorize -fno-honor-nans";; esac
+  /opt/rocm/bin/hipcc $FL $extra -c "$f" -o $B/$(basename $f).o &
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $B/*.o -o "$ROOT/video-blade_amd/vblade/variants/lib_$TAG.so"
+echo "built variants/lib_$TAG.so"

@@ -217,10 +217,11 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     vpbase = reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1]);
   }
 
-  auto tile_src = [&](int t) __attribute__((always_inline)) -> TileSrc {
+  // where tile t's keys come from; `blk_raw` = list[t >> 1] (read ahead by the caller)
+  auto tile_src = [&](int t, int blk_raw) __attribute__((always_inline)) -> TileSrc {
     TileSrc s;
     if (t < ntm) {
-      const int blk = __builtin_amdgcn_readfirstlane(list[t >> 1]);  // provably wave-uniform
+      const int blk = __builtin_amdgcn_readfirstlane(blk_raw);  // provably wave-uniform
       s.pooled = 0;
       s.kstart = blk * kQBlk + (t & 1) * kKT;
       s.klen = min(kKT, Lk - s.kstart);
@@ -273,8 +274,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     my_voff[i] = my_row[i] * my_rowb + my_chunk[i] * 16;
     my_pvoff[i] = my_row[i] * my_prowb + my_chunk[i] * 16;
   }
-  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
-    const TileSrc src = tile_src(t);
+  auto issue = [&](const TileSrc src, int slot) __attribute__((always_inline)) {
     uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
     const bool pooled = kPool && src.pooled;
     if (kKvRows && !pooled) {   // gathered k/v rows (generic API path; serialises the ring)
@@ -353,8 +353,8 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       const int row0 = (kk >> 1) * 32 + 16 * (kk & 1);   // + vrow (in v_lane)
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        vlo[kk][dt] = lds_tr4_imm(v_lane[dt], kSlot * kBufBytes + kMatBytes + row0 * kRowB);
-        vhi[kk][dt] = lds_tr4_imm(v_lane[dt], kSlot * kBufBytes + kMatBytes + (row0 + 8) * kRowB);
+        vlo[kk][dt] = lds_tr4_asm(v_lane[dt], kSlot * kBufBytes + kMatBytes + row0 * kRowB);
+        vhi[kk][dt] = lds_tr4_asm(v_lane[dt], kSlot * kBufBytes + kMatBytes + (row0 + 8) * kRowB);
       }
     };
     auto wait_v = [&](int kk) __attribute__((always_inline)) {
@@ -437,11 +437,25 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     VB_ACC(4, s3 - s2);
   };
 
-  for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t, t);
+  // Each ring slot remembers its tile's source (SGPRs, written when the tile is issued), and the
+  // kept-block index of the next tile to issue is read from LDS one tile ahead, so no LDS round
+  // trip sits between a barrier and the tile's first MFMA.
+  auto list_at = [&](int t) __attribute__((always_inline)) -> int {
+    return t < ntm ? (int)list[min(t >> 1, kMaxBlocks - 1)] : 0;
+  };
+  TileSrc slot_src[kBufs];
+  slot_src[0] = tile_src(0, list_at(0));
+  if (ntiles > 0) issue(slot_src[0], 0);
+  if constexpr (kBufs > 2) {
+    slot_src[1] = tile_src(1, list_at(1));
+    if (ntiles > 1) issue(slot_src[1], 1);
+  }
+  int next_blk = list_at(kBufs - 1);
   // The loop body is instantiated once per ring slot (compile-time U), so every LDS address is a
   // loop-invariant lane base + immediate offset: no address VALU inside the loop.
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
+    constexpr int un = (u + kBufs - 1) % kBufs;   // slot of the tile issued during this one
     VB_STAMP(st0);
     // retire this wave's DMAs of tile t (younger tiles stay in flight); the barrier then makes
     // every wave's part visible and proves slot (t-1) % kBufs is no longer being read
@@ -453,10 +467,15 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     __builtin_amdgcn_s_barrier();
     VB_STAMP(st1);
     VB_ACC(0, st1 - st0);
-    if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1, (u + kBufs - 1) % kBufs);
+    const int ti = t + kBufs - 1;
+    if (ti < ntiles) {
+      slot_src[un] = tile_src(ti, next_blk);
+      issue(slot_src[un], un);
+      next_blk = list_at(ti + 1);   // in flight during this tile's compute
+    }
     VB_STAMP(st2);
     VB_ACC(1, st2 - st1);
-    const TileSrc src = tile_src(t);
+    const TileSrc src = slot_src[u];
     const float bias = (kPool && src.pooled) ? p.pool_bias_l2 : 0.f;
     if (VB_DIAG && (p.dbg & 2)) return;   // diagnostic: stream tiles only
     tile_step(U, bias, src.klen);
@@ -478,8 +497,10 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
 
   // ---- epilogue -----------------------------------------------------------------------------------
   const float lt = add_xor32(l);
-  float inv = (lt > 0.f) ? 1.0f / lt : 0.f;
-  if (nan_head) inv = __builtin_nanf("");
+  const float inv = (lt > 0.f) ? 1.0f / lt : 0.f;
+  // streaming heads (unsupported) are flagged with NaN outputs written as bit patterns: this
+  // translation unit is compiled with -fno-honor-nans, so no float arithmetic may produce them
+  constexpr uint32_t kNaN2 = std::is_same<T, BF16>::value ? 0x7FC07FC0u : 0x7E007E00u;
   if (qvalid) {
     uint8_t* obase = reinterpret_cast<uint8_t*>(p.out) +
                      2 * (b * p.os[0] + h * p.os[1] + (qrow0 + qrow) * p.os[2]);
@@ -491,12 +512,14 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
         u32x2 w;
         w[0] = pack2<T>(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
         w[1] = pack2<T>(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+        if (nan_head) w[0] = w[1] = kNaN2;
         *reinterpret_cast<u32x2*>(obase + d * 2) = w;
       }
     if (p.lse && half == 0) {
-      float v = (m + __log2f(lt)) * kLn2;
-      if (nan_head) v = __builtin_nanf("");
-      p.lse[b * p.lse_s[0] + h * p.lse_s[1] + (p.cu_q ? qg : qrow)] = v;
+      const float v = (m + __log2f(lt)) * kLn2;
+      float* dst = p.lse + b * p.lse_s[0] + h * p.lse_s[1] + (p.cu_q ? qg : qrow);
+      if (nan_head) *reinterpret_cast<uint32_t*>(dst) = 0x7FC00000u;
+      else *dst = v;
     }
   }
 }

@@ -22,20 +22,22 @@ __device__ __forceinline__ typename T::vec8 lds_b128(const uint8_t* base, int of
   return *reinterpret_cast<const typename T::vec8*>(base + off);
 }
 
-// ds_read_b64_tr_b16 issued from inline asm: hipcc's waitcnt pass treats the builtin form as
-// possibly aliasing in-flight LDS-DMA writes and drains the whole DMA queue (vmcnt(0)) before it.
-// The asm form is invisible to that pass, so its result must be waited for explicitly (a
-// `s_waitcnt lgkmcnt(0)` asm that names the destinations) before any use.
+// ds_read_b64_tr_b16, two forms:
+//  * lds_tr4 / lds_tr4_imm: the compiler builtin. hipcc's hazard recognizer and waitcnt pass see
+//    it; but while LDS-DMA writes are in flight the waitcnt pass drains the whole DMA queue
+//    (s_waitcnt vmcnt(0)) before it, serialising a DMA ring.
+//  * lds_tr4_asm: inline asm, invisible to the waitcnt pass. Its destination is NOT ready when the
+//    statement returns: wait with an `s_waitcnt lgkmcnt` asm that names the destinations before any
+//    use. Only its result is asm-produced; it reads no MFMA result, so no MFMA->VALU hazard applies.
 __device__ __forceinline__ s16x4 lds_tr4(const uint8_t* base, int off) {
-  const uint32_t a = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)(base + off)));
-  s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return r;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(base + off));
 }
-
-// the same with a compile-time immediate offset on a loop-invariant lane address
 __device__ __forceinline__ s16x4 lds_tr4_imm(uint32_t lane_addr, int imm) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      reinterpret_cast<__attribute__((address_space(3))) s16x4*>(static_cast<uintptr_t>(lane_addr + imm)));
+}
+__device__ __forceinline__ s16x4 lds_tr4_asm(uint32_t lane_addr, int imm) {
   s16x4 r;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lane_addr), "i"(imm));
   return r;
@@ -58,13 +60,11 @@ __device__ __forceinline__ typename T::vec8 pack8(const f32x16& acc, int base) {
   return __builtin_bit_cast(typename T::vec8, u);
 }
 
-// max of three floats as ONE v_max3_f32. Through fmaxf hipcc first canonicalises every MFMA
-// result with a v_max x,x (IEEE sNaN quieting): an extra VALU per score on the softmax path.
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// max of three floats: one v_max3_f32 when the translation unit is built with -fno-honor-nans
+// (see the Makefile; otherwise hipcc canonicalises every MFMA result with an extra v_max x,x).
+// Never inline asm here: an asm statement reading MFMA results is invisible to hipcc's hazard
+// recognizer, which then omits the wait states between the MFMA write and the read.
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
 // ---- LDS-DMA through a buffer descriptor ------------------------------------------------------------
 // (base, extent) of a wave-uniform buffer; the descriptor itself is built inside dma16 (the compiler
