@@ -55,6 +55,10 @@ constexpr int kThreads = 256;
 constexpr int kQBlk = 128;   // rows per workgroup (4 waves x 32)
 constexpr int kKT = 64;      // keys per LDS tile
 constexpr int kMaxBlocks = 1024;  // keys <= 131072
+#ifndef VB_RESCALE_SLACK
+#define VB_RESCALE_SLACK 4.0f
+#endif
+constexpr float kRescaleSlack = VB_RESCALE_SLACK;  // log2 units: P <= 16 between rescales
 
 // ---- LDS images --------------------------------------------------------------------------------
 // K: [64 rows][D] with 16-byte chunks XOR-swizzled so a ds_read_b128 column slice (32 rows, one
@@ -385,9 +389,12 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     const float f2 = max3f(mq[2], mq[3], s[0][15]);
     float mt = max3f(max3f(f1, f2, s[1][7]), s[1][15], s[1][15]);
     mt = max_xor32(mt) * p.c + bias;            // tile row max, exp2 domain
-    // lazy rescale: only when some row's running max grows (exact; no threshold). The empty
-    // volatile asm keeps hipcc from if-converting this rare block into every iteration.
-    if (!__all(mt <= m)) {
+    // Deferred rescale (guide T13): the running max m is raised only when some row's tile max
+    // exceeds it by more than kRescaleSlack (log2 units), so P = exp2(s - m) <= 2^kRescaleSlack.
+    // O and l always share the same m, so the result is exact up to rounding; without the slack
+    // nearly every tile of a 32-row wave rescales (some row's max grows), a 40-VALU O-wide pass.
+    // The empty volatile asm keeps hipcc from if-converting this block into every iteration.
+    if (!__all(mt <= m + kRescaleSlack)) {
       asm volatile("");
       const float mn = fmaxf(m, mt);
       const float alpha = exp2_fast(m - mn);
