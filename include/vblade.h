@@ -126,7 +126,11 @@ typedef struct vb_predict_args {
   uint8_t* mask;           /* [B,H,nb,nb] contiguous */
   unsigned long long* mask_count; /* nullable */
   int dtype;
+  void* workspace;         /* device, 16-byte aligned, >= vb_mask_predict_workspace_size(args) bytes:
+                              the sampled q/k rows staged contiguously */
+  uint64_t workspace_bytes;
 } vb_predict_args;
+uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);
 
 /* Energy rule alone on given scores (transfer_attn_to_mask, mode="energy"):

@@ -23,7 +23,11 @@ def load(tag):
     path = os.path.join(ROOT, "video-blade_amd", "vblade", "variants", f"lib_{tag}.so")
     lib = ctypes.CDLL(path)
     for name, (res, args) in _lib.SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:   # an older ABI: entry points it predates become no-op stubs
+            setattr(lib, name, lambda *a: 0)
+            continue
         fn.restype, fn.argtypes = res, args
     return lib
 

@@ -14,7 +14,7 @@
 // Nothing but Po and the mask reaches HBM (R stays in LDS).
 #include <cstdlib>
 
-#include "vb_common.hpp"
+#include "vb_tiles.hpp"
 
 namespace vb {
 
@@ -26,6 +26,7 @@ constexpr int kKeysPerTile = 64;   // two 32-key sampled blocks per LDS tile
 struct PredParams {
   const void* q; const void* k;
   int64_t qs[3], ks[3];
+  uint8_t* q_s; uint8_t* k_s;   // sampled rows [B,H,nb*32,D] contiguous (workspace)
   const int32_t* rows;
   const int32_t* q_off; const int32_t* k_off;
   int B, H, L, D, block, nb;
@@ -144,8 +145,30 @@ __device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int n
   return kept;
 }
 
-// s_waitcnt vmcnt(n) with lgkm/exp counters left at max (gfx9 encoding)
-#define VB_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
+// Sampled rows of q and k, gathered once into contiguous [B,H,nb*32,D] (blockIdx.y: 0 = q, 1 = k):
+// row j*32 + t of (b,h) = reordered position min(j*block + off[b,h,t], L-1) (replicate padding),
+// read at the caller's row rows[pos]. The predictor then streams K by plain LDS-DMA.
+template <class T>
+__global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
+  const int CH = p.D / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nrow = (int64_t)p.nb * 32;
+  if (idx >= (int64_t)p.B * p.H * nrow * CH) return;
+  const bool isk = blockIdx.y != 0;
+  const int ch = idx % CH;
+  const int64_t r = idx / CH;
+  const int jt = r % nrow;
+  const int bh = r / nrow;
+  const int b = bh / p.H, h = bh % p.H;
+  const int32_t* off = (isk ? p.k_off : p.q_off) + (int64_t)bh * 32;
+  int pos = min((jt >> 5) * p.block + off[jt & 31], p.L - 1);
+  if (p.rows) pos = p.rows[pos];
+  const int64_t* st = isk ? p.ks : p.qs;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(isk ? p.k : p.q) +
+                       2 * (b * st[0] + h * st[1] + (int64_t)pos * st[2]) + ch * 16;
+  uint8_t* dst = (isk ? p.k_s : p.q_s) + (r * p.D + ch * 8) * 2;
+  *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+}
 
 template <int D, class T>
 __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredParams p) {
@@ -155,58 +178,54 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   constexpr int kRowsPerInst = 1024 / kRowB;          // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerWave = kTileBytes / 1024 / kPWaves;
   constexpr int kBufs = 4;                            // tiles t (read), t+1, t+2 in flight, t+3 issued
-  // LDS: R [4 waves][32 rows][rstride] storage dtype | m [4][32] f32 | sampled-key row table
-  //      [nb][32] u16 | K tiles x4 (after the main loop: per-wave row scratch)
+  // LDS: R [4 waves][32 rows][rstride] storage dtype | m [4][32] f32 | K tiles x4 (after the main
+  //      loop: per-wave row scratch)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nb = p.nb;
   const int rstride = (nb + 7) & ~7;
   typename T::raw* R = reinterpret_cast<typename T::raw*>(smem);
   const int r_bytes = (kPWaves * 32 * rstride * 2 + 15) & ~15;
   float* mrow_s = reinterpret_cast<float*>(smem + r_bytes);
-  uint16_t* krow = reinterpret_cast<uint16_t*>(smem + r_bytes + kPWaves * 32 * 4);
-  uint8_t* ktile = smem + r_bytes + kPWaves * 32 * 4 + ((nb * 32 * 2 + 15) & ~15);
+  uint8_t* ktile = smem + r_bytes + kPWaves * 32 * 4;
   float* rowbuf = reinterpret_cast<float*>(ktile);  // [4][2][kMaxNb + 4], reused after the loop
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int half = lane >> 5;
   const int l32 = lane & 31;
-  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 share one),
-  // so give each XCD a contiguous range of (head, q-group) work — a head's sampled keys are then
-  // re-read from that XCD's own L2 instead of the Infinity Cache. Placement only affects speed.
+  // XCD-aware order: give each XCD a contiguous range of (head, q-group) work, so a head's sampled
+  // keys are re-read from that XCD's own L2. Placement only affects speed.
   const int nqg = (nb + kPWaves - 1) / kPWaves;
-  const int nwg = nqg * p.B * p.H;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int lin = xcd_linear(blockIdx.x, nqg * p.B * p.H);
   const int bh = lin / nqg;
-  const int b = bh / p.H, h = bh % p.H;
   const int qb = (lin % nqg) * kPWaves + wave;  // this wave's sampled q-block
   const bool wave_active = qb < nb;
-
-  const uint8_t* qbase = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1]);
-  const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1]);
-  const int64_t kstride_b = 2 * p.ks[2];
-  const int32_t* qoff = p.q_off + (int64_t)bh * 32;
-  const int32_t* koff = p.k_off + (int64_t)bh * 32;
-
-  // caller rows of every sampled key (block j, slot t): one parallel gather, then LDS lookups
-  for (int e = threadIdx.x; e < nb * 32; e += kPThreads)
-    krow[e] = (uint16_t)sampled_row(e >> 5, koff[e & 31], p.block, p.L, p.rows);
+  const int64_t slice = (int64_t)nb * 32 * kRowB;   // bytes of one (b,h) sampled stream
 
   // Q fragment of this lane's sampled row (B operand of S^T = K_s . Q_s^T)
   typename T::vec8 qf[KS];
   {
-    const int row = sampled_row(wave_active ? qb : 0, qoff[l32], p.block, p.L, p.rows);
-    const uint8_t* qp = qbase + (int64_t)row * 2 * p.qs[2];
+    const uint8_t* qp = p.q_s + bh * slice + (int64_t)((wave_active ? qb : 0) * 32 + l32) * kRowB;
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
 #pragma unroll
     for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]));  // see vb_attn_fwd.hip
   }
+  // K tiles by LDS-DMA from the contiguous sampled stream: a buffer descriptor per (b,h), each
+  // lane's fixed (row, swizzled chunk) as voffset, the tile's first row as soffset. Rows past the
+  // stream (odd nb: the last tile's second block) read as zeros and are never used.
+  const srd_t ksrd = make_srd(p.k_s + bh * slice, (int)slice);
+  int voff[kInstPerWave];
+#pragma unroll
+  for (int i = 0; i < kInstPerWave; ++i) {
+    const int r = (wave * kInstPerWave + i) * kRowsPerInst + lane / (kRowB / 16);
+    const int sl = lane % (kRowB / 16);
+    const int sw = (D == 64) ? ((r >> 1) & 7) : (r & 15);
+    voff[i] = r * kRowB + 16 * (sl ^ sw);
+  }
   float m = -INFINITY;
-  __syncthreads();   // krow visible; all plain global loads retired before the DMA pipeline
+  __syncthreads();   // all plain global loads retired before the DMA pipeline
 
   const int ntiles = (VB_DIAG && (p.dbg & 2)) ? 0 : (nb + 1) / 2;
   // K tile t by LDS-DMA (global_load_lds_dwordx4): the LDS image is written linearly (1 KiB per
@@ -215,16 +234,8 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   auto issue = [&](int t) {
     uint8_t* dst = ktile + (t % kBufs) * kTileBytes;
 #pragma unroll
-    for (int i = 0; i < kInstPerWave; ++i) {
-      const int inst = wave * kInstPerWave + i;
-      const int r = inst * kRowsPerInst + lane / (kRowB / 16);       // key row within the tile
-      const int sl = lane % (kRowB / 16);
-      const int sw = (D == 64) ? ((r >> 1) & 7) : (r & 15);
-      const int blk = min(2 * t + (r >> 5), nb - 1);
-      const uint8_t* src = kbase + (int64_t)krow[blk * 32 + (r & 31)] * kstride_b + 16 * (sl ^ sw);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(dst + inst * 1024), 16, 0, 0);
-    }
+    for (int i = 0; i < kInstPerWave; ++i)
+      dma16(ksrd, dst + (wave * kInstPerWave + i) * 1024, voff[i], t * kTileBytes);
   };
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
   for (int t = 0; t < ntiles; ++t) {
@@ -410,7 +421,12 @@ static size_t predict_smem_bytes(int nb, int D) {
   const size_t r_bytes = ((size_t)kPWaves * 32 * rstride * 2 + 15) & ~size_t(15);
   const size_t tiles = 4 * (size_t)kKeysPerTile * D * 2;
   const size_t scratch = (size_t)kPWaves * 2 * (kMaxNb + 4) * 4;
-  return r_bytes + kPWaves * 32 * 4 + (((size_t)nb * 32 * 2 + 15) & ~size_t(15)) + (tiles > scratch ? tiles : scratch);
+  return r_bytes + kPWaves * 32 * 4 + (tiles > scratch ? tiles : scratch);
+}
+
+static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
+  const int nb = (L + 127) / 128;
+  return 2 * ((uint64_t)B * H * nb * 32 * D * 2);
 }
 
 template <int D, class T>
@@ -420,12 +436,20 @@ static int launch_predict(const PredParams& p, hipStream_t stream) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)smem) != hipSuccess)
     return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
+  const int64_t gthreads = (int64_t)p.B * p.H * p.nb * 32 * (D / 8);
+  hipLaunchKernelGGL(sample_rows_kernel<T>, dim3((unsigned)((gthreads + 255) / 256), 2), dim3(256), 0, stream, p);
+  if (int rc = check_launch("sample_rows_kernel")) return rc;
   const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
   return check_launch("mask_predict_kernel");
 }
 
 }  // namespace vb
+
+extern "C" uint64_t vb_mask_predict_workspace_size(const vb_predict_args* a) {
+  if (!a || a->B <= 0 || a->H <= 0 || a->L <= 0 || a->D <= 0) return 0;
+  return vb::predict_ws_bytes(a->B, a->H, a->L, a->D);
+}
 
 extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   using namespace vb;
@@ -438,6 +462,11 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   if (nb > kMaxNb) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: sequence too long");
   if (a->L > 65535) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: L must be < 65536");
   if (a->min_keep < 1 || a->max_keep < 1) return fail(VB_ERR_INVALID, "vb_mask_predict: keep counts must be >= 1");
+  if (a->D != 64 && a->D != 128) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: head_dim must be 64 or 128");
+  const uint64_t ws = predict_ws_bytes(a->B, a->H, a->L, a->D);
+  if (!a->workspace || a->workspace_bytes < ws || (reinterpret_cast<uintptr_t>(a->workspace) & 15))
+    return fail(VB_ERR_INVALID, "vb_mask_predict: workspace missing or smaller than vb_mask_predict_workspace_size()");
+  if (ws / 2 / a->B / a->H >= (uint64_t(1) << 31)) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: sampled stream too large");
   for (int i = 0; i < 3; ++i)
     if ((a->q_stride[i] | a->k_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_mask_predict: strides must be multiples of 8");
   PredParams p{};
@@ -450,6 +479,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   p.thr = a->energy_threshold;
   p.min_keep = a->min_keep; p.max_keep = a->max_keep; p.force_tail = a->force_tail;
   p.po = a->po; p.mask = a->mask; p.count = a->mask_count;
+  p.q_s = reinterpret_cast<uint8_t*>(a->workspace);
+  p.k_s = p.q_s + ws / 2;
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);
 #endif

@@ -52,6 +52,7 @@ class PredictArgs(ctypes.Structure):
         ("min_keep", ctypes.c_int), ("max_keep", ctypes.c_int), ("force_tail", ctypes.c_int),
         ("po", _vp), ("mask", _vp), ("mask_count", _vp),
         ("dtype", ctypes.c_int),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_uint64),
     ]
 
 
@@ -92,6 +93,7 @@ SIGNATURES = {
         ctypes.c_float, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         _vp, _vp, _vp]),
     "vb_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnArgs), _vp]),
+    "vb_mask_predict_workspace_size": (ctypes.c_uint64, [ctypes.POINTER(PredictArgs)]),
     "vb_mask_predict": (ctypes.c_int, [ctypes.POINTER(PredictArgs), _vp]),
     "vb_energy_mask": (ctypes.c_int, [
         _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,

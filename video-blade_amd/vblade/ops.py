@@ -303,7 +303,11 @@ def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_ke
     a.min_keep, a.max_keep, a.force_tail = int(min_keep), int(max_keep), int(force_tail)
     a.po, a.mask, a.mask_count = po.data_ptr(), mask.data_ptr(), _ptr(mask_count)
     a.dtype = _dtype_code(q)
-    check(_lib.load().vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
+    lib = _lib.load()
+    nbytes = int(lib.vb_mask_predict_workspace_size(ctypes.byref(a)))
+    ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
+    check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
 
 
