@@ -1,4 +1,4 @@
-// Mask predictor, mean pooling and the reference-faithful LSE combine for gfx950.
+// Mask predictor for gfx950 (sampled pooled scores + energy top-k).
 //
 // vb_mask_predict fuses, per (b, h) and group of four 32-row sampled q-blocks:
 //   * efficient_attn_with_pooling: replicate pad + per-block token sampling
@@ -13,6 +13,8 @@
 //     crossing of storage(total * thr), clamp to [min_keep, max_keep], forced tail rows/cols.
 // Nothing but Po and the mask reaches HBM (R stays in LDS).
 #include <cstdlib>
+
+#include <type_traits>
 
 #include "vb_tiles.hpp"
 
@@ -65,10 +67,9 @@ __device__ __forceinline__ uint32_t storage_bits(float v) {
 // first (a stable descending sort), one unsigned compare per pair. The fp32-accumulated
 // cumulative sum over the sorted values runs sequentially (bit-identical to torch's CPU cumsum)
 // through v_readlane on a register-distributed copy, recording each prefix in its own lane.
-template <class T>
-__device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
-                          int min_keep, int max_keep, int force_cols, bool force_all) {
-  constexpr int U = kMaxNb / 64 + 1;
+template <class T, int U>
+__device__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
+                            int min_keep, int max_keep, int force_cols, bool force_all) {
   const int lane = threadIdx.x & 63;
   uint32_t mykey[U];
   int rank[U];
@@ -143,6 +144,19 @@ __device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int n
   }
   for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
   return kept;
+}
+// U = values per lane, the smallest that covers the row (ranks cost nc * U compares per lane)
+template <class T>
+__device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
+                          int min_keep, int max_keep, int force_cols, bool force_all) {
+  switch ((nc + 63) >> 6) {
+    case 1: return energy_row_u<T, 1>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols, force_all);
+    case 2: return energy_row_u<T, 2>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols, force_all);
+    case 3: return energy_row_u<T, 3>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols, force_all);
+    case 4: return energy_row_u<T, 4>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols, force_all);
+    default: return energy_row_u<T, (kMaxNb + 63) / 64>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols,
+                                                           force_all);
+  }
 }
 
 // Sampled rows of q and k, gathered once into contiguous [B,H,nb*32,D] (blockIdx.y: 0 = q, 1 = k):
@@ -231,14 +245,24 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   // K tile t by LDS-DMA (global_load_lds_dwordx4): the LDS image is written linearly (1 KiB per
   // wave-instruction), so the 16-byte-chunk XOR swizzle of the image is applied to each lane's
   // SOURCE address: LDS slot `sl` of row r holds chunk sl ^ sw(r).
-  auto issue = [&](int t) {
+  auto issue = [&](int t) __attribute__((always_inline)) {
     uint8_t* dst = ktile + (t % kBufs) * kTileBytes;
 #pragma unroll
     for (int i = 0; i < kInstPerWave; ++i)
       dma16(ksrd, dst + (wave * kInstPerWave + i) * 1024, voff[i], t * kTileBytes);
   };
+  // loop-invariant lane addresses of the K fragment reads (the swizzle depends on the lane's row
+  // bits only), so every read of every slot is base + compile-time immediate
+  int k_lane[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int sw = (D == 64) ? ((l32 >> 1) & 7) : (l32 & 15);
+    k_lane[ks] = l32 * kRowB + 16 * ((2 * ks + half) ^ sw);
+  }
+  typename T::raw* Rrow = R + (wave * 32 + l32) * rstride;
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
-  for (int t = 0; t < ntiles; ++t) {
+  auto body = [&](int t, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
     // retire this wave's DMA of tile t (younger tiles stay in flight), then the barrier makes
     // every wave's part visible and guarantees tile t-1's buffer is no longer being read
     const int younger = min(ntiles - 1 - t, kBufs - 2);
@@ -247,32 +271,38 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     else VB_WAIT_VMCNT(0);
     __builtin_amdgcn_s_barrier();
     if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
-    const uint8_t* kl = ktile + (t % kBufs) * kTileBytes;
+    const uint8_t* kl = ktile + u * kTileBytes;
+    float mx[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
-      const int j = 2 * t + kt;
       typename T::vec8 kf[KS];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int row = kt * 32 + l32;
-        const int sw = (D == 64) ? ((row >> 1) & 7) : (row & 15);
-        kf[ks] = *reinterpret_cast<const typename T::vec8*>(kl + row * kRowB + 16 * ((2 * ks + half) ^ sw));
-      }
-      f32x16 s;
+      for (int ks = 0; ks < KS; ++ks)
+        kf[ks] = *reinterpret_cast<const typename T::vec8*>(kl + kt * 32 * kRowB + k_lane[ks]);
+      f32x16 sc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+      for (int r = 0; r < 16; ++r) sc[r] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s = T::mfma32(kf[ks], qf[ks], s);
-      float mx = fmaxf(s[0], s[1]);
+      for (int ks = 0; ks < KS; ++ks) sc = T::mfma32(kf[ks], qf[ks], sc);
+      float x = fmaxf(fmaxf(sc[0], sc[1]), sc[2]);
 #pragma unroll
-      for (int r = 2; r < 16; ++r) mx = fmaxf(mx, s[r]);
-      mx = max_xor32(mx) * p.c;                       // tl.max(qk, 1) * qk_scale
-      if (j < nb) {
-        m = fmaxf(m, mx);
-        if (half == kt) R[(wave * 32 + l32) * rstride + j] = T::from_f32(mx);
-      }
+      for (int r = 3; r < 15; r += 2) x = fmaxf(fmaxf(x, sc[r]), sc[r + 1]);
+      x = fmaxf(x, sc[15]);
+      mx[kt] = max_xor32(x) * p.c;                   // tl.max(qk, 1) * qk_scale
     }
+    // half 0 stores block 2t, half 1 block 2t+1 (both halves hold both row maxima)
+    const int j = 2 * t + half;
+    const bool second = 2 * t + 1 < nb;
+    m = fmaxf(m, second ? fmaxf(mx[0], mx[1]) : mx[0]);
+    if (j < nb) Rrow[j] = T::from_f32(half ? mx[1] : mx[0]);
+  };
+  for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
+    body(t0, std::integral_constant<int, 0>{});
+    if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
+    if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
+    if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
   }
+  static_assert(kBufs == 4, "the loop body is instantiated once per ring slot");
   if (half == 0) mrow_s[wave * 32 + l32] = m;
   __syncthreads();
   if (!wave_active || (VB_DIAG && (p.dbg & 1))) return;
@@ -326,94 +356,6 @@ __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int ro
   const int kept = energy_row<T>(val, reinterpret_cast<uint32_t*>(val + kMaxNb + 4), mask + (int64_t)row * nc, nc,
                                  thr, min_keep, max_keep, force_tail, force_all);
   if (count && lane == 0) atomicAdd(count, (unsigned long long)kept);
-}
-
-// simple_pooling of K and V: one thread per 16-byte chunk of a pooled row. Every reordered row
-// is read by exactly one thread, which (when k_r/v_r are given) also writes it to the contiguous
-// Gilbert-ordered copies the attention kernel streams (the reference's index_select, fused).
-template <class T>
-__global__ void __launch_bounds__(256) pool_kv_kernel(const uint8_t* k, const uint8_t* v, int64_t ks0, int64_t ks1,
-                                                      int64_t ks2, int64_t vs0, int64_t vs1, int64_t vs2,
-                                                      const int32_t* rows, int B, int H, int L, int D, int gap,
-                                                      int Lp, uint8_t* kp, uint8_t* vp, uint8_t* k_r,
-                                                      uint8_t* v_r) {
-  const int CH = D / 8;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)B * H * Lp * CH;
-  if (idx >= total) return;
-  const int ch = idx % CH;
-  const int64_t prow = idx / CH;        // (b*H + h)*Lp + pr
-  const int pr = prow % Lp;
-  const int bh = prow / Lp;
-  const int b = bh / H, h = bh % H;
-  float ak[8], av[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ak[e] = av[e] = 0.f;
-  for (int t = 0; t < gap; ++t) {
-    const int g = pr * gap + t;
-    int pos = min(g, L - 1);  // replicate padding
-    if (rows) pos = rows[pos];
-    const u32x4 xk = *reinterpret_cast<const u32x4*>(k + 2 * (b * ks0 + h * ks1 + (int64_t)pos * ks2) + ch * 16);
-    const u32x4 xv = *reinterpret_cast<const u32x4*>(v + 2 * (b * vs0 + h * vs1 + (int64_t)pos * vs2) + ch * 16);
-    if (k_r && g < L) {
-      const int64_t o = ((int64_t)bh * L + g) * D * 2 + ch * 16;
-      *reinterpret_cast<u32x4*>(k_r + o) = xk;
-      *reinterpret_cast<u32x4*>(v_r + o) = xv;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      ak[2 * e] += T::bits_to_f32(xk[e] & 0xffff);
-      ak[2 * e + 1] += T::bits_to_f32(xk[e] >> 16);
-      av[2 * e] += T::bits_to_f32(xv[e] & 0xffff);
-      av[2 * e + 1] += T::bits_to_f32(xv[e] >> 16);
-    }
-  }
-  const float f = 1.0f / (float)gap;  // mean = sum * (1/N), as ATen's MeanOps
-  u32x4 ok, ov;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    ok[e] = pack2<T>(ak[2 * e] * f, ak[2 * e + 1] * f);
-    ov[e] = pack2<T>(av[2 * e] * f, av[2 * e + 1] * f);
-  }
-  *reinterpret_cast<u32x4*>(kp + (prow * D + ch * 8) * 2) = ok;
-  *reinterpret_cast<u32x4*>(vp + (prow * D + ch * 8) * 2) = ov;
-}
-
-// adaptive_block_sparse_attn's combine (cogvideo_blocksparseattn.py:374-393), eager-op rounding
-template <class T>
-__global__ void __launch_bounds__(256) lse_combine_kernel(const uint8_t* out1, const float* lse1, const uint8_t* out2,
-                                                          const float* lse2, int64_t rows, int D, float gap,
-                                                          uint8_t* out, float* alpha_out) {
-  const int CH = D / 8;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * CH) return;
-  const int64_t row = idx / CH;
-  const int ch = idx % CH;
-  const float l1 = round_to<T>(lse1[row]);
-  const float l2 = round_to<T>(lse2[row]);
-  const float log_g = round_to<T>(logf(round_to<T>(gap)));
-  const float w2 = round_to<T>(l2 + log_g);
-  const float mx = fmaxf(l1, w2);
-  const float e1 = round_to<T>(expf(round_to<T>(l1 - mx)));
-  const float e2 = round_to<T>(expf(round_to<T>(w2 - mx)));
-  const float a = round_to<T>(e1 / round_to<T>(e1 + e2));
-  const float b = round_to<T>(1.0f - a);
-  if (alpha_out && ch == 0) alpha_out[row] = a;
-  const u32x4 x1 = *reinterpret_cast<const u32x4*>(out1 + (row * D + ch * 8) * 2);
-  const u32x4 x2 = *reinterpret_cast<const u32x4*>(out2 + (row * D + ch * 8) * 2);
-  u32x4 y;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float r[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const float v1 = T::bits_to_f32((x1[e] >> (16 * s)) & 0xffff);
-      const float v2 = T::bits_to_f32((x2[e] >> (16 * s)) & 0xffff);
-      r[s] = round_to<T>(round_to<T>(v1 * a) + round_to<T>(v2 * b));
-    }
-    y[e] = pack2<T>(r[0], r[1]);
-  }
-  *reinterpret_cast<u32x4*>(out + (row * D + ch * 8) * 2) = y;
 }
 
 static size_t predict_smem_bytes(int nb, int D) {
@@ -517,54 +459,4 @@ extern "C" int vb_energy_mask(const void* po, int B, int H, int nr, int nc, floa
   else
     return fail(VB_ERR_INVALID, "vb_energy_mask: unknown dtype");
   return check_launch("energy_mask_kernel");
-}
-
-extern "C" int vb_pool_kv(const void* k, const void* v, const int64_t* k_stride, const int64_t* v_stride,
-                          const int32_t* rows, int B, int H, int L, int D, int gap, int dtype, void* kp, void* vp,
-                          void* k_r, void* v_r, void* stream) {
-  using namespace vb;
-  if (!k || !v || !k_stride || !v_stride || !kp || !vp) return fail(VB_ERR_INVALID, "vb_pool_kv: null argument");
-  if ((k_r == nullptr) != (v_r == nullptr)) return fail(VB_ERR_INVALID, "vb_pool_kv: give both k_r and v_r or neither");
-  if (B <= 0 || H <= 0 || L <= 0 || gap <= 0 || D % 8) return fail(VB_ERR_INVALID, "vb_pool_kv: bad sizes");
-  for (int i = 0; i < 3; ++i)
-    if ((k_stride[i] | v_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_pool_kv: strides must be multiples of 8");
-  const int Lp = (L + gap - 1) / gap;
-  const int64_t total = (int64_t)B * H * Lp * (D / 8);
-  const dim3 grid((unsigned)((total + 255) / 256));
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  auto* kb = reinterpret_cast<const uint8_t*>(k);
-  auto* vb_ = reinterpret_cast<const uint8_t*>(v);
-  if (dtype == VB_DTYPE_BF16)
-    hipLaunchKernelGGL(pool_kv_kernel<BF16>, grid, dim3(256), 0, s, kb, vb_, k_stride[0], k_stride[1], k_stride[2],
-                       v_stride[0], v_stride[1], v_stride[2], rows, B, H, L, D, gap, Lp,
-                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp),
-                       reinterpret_cast<uint8_t*>(k_r), reinterpret_cast<uint8_t*>(v_r));
-  else if (dtype == VB_DTYPE_F16)
-    hipLaunchKernelGGL(pool_kv_kernel<F16>, grid, dim3(256), 0, s, kb, vb_, k_stride[0], k_stride[1], k_stride[2],
-                       v_stride[0], v_stride[1], v_stride[2], rows, B, H, L, D, gap, Lp,
-                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp),
-                       reinterpret_cast<uint8_t*>(k_r), reinterpret_cast<uint8_t*>(v_r));
-  else
-    return fail(VB_ERR_INVALID, "vb_pool_kv: unknown dtype");
-  return check_launch("pool_kv_kernel");
-}
-
-extern "C" int vb_lse_combine(const void* out1, const float* lse1, const void* out2, const float* lse2, int B, int H,
-                              int L, int D, float gap, int dtype, void* out, float* alpha, void* stream) {
-  using namespace vb;
-  if (!out1 || !lse1 || !out2 || !lse2 || !out) return fail(VB_ERR_INVALID, "vb_lse_combine: null argument");
-  if (B <= 0 || H <= 0 || L <= 0 || D % 8) return fail(VB_ERR_INVALID, "vb_lse_combine: bad sizes");
-  const int64_t rows = (int64_t)B * H * L;
-  const dim3 grid((unsigned)((rows * (D / 8) + 255) / 256));
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  auto* o1 = reinterpret_cast<const uint8_t*>(out1);
-  auto* o2 = reinterpret_cast<const uint8_t*>(out2);
-  auto* o = reinterpret_cast<uint8_t*>(out);
-  if (dtype == VB_DTYPE_BF16)
-    hipLaunchKernelGGL(lse_combine_kernel<BF16>, grid, dim3(256), 0, s, o1, lse1, o2, lse2, rows, D, gap, o, alpha);
-  else if (dtype == VB_DTYPE_F16)
-    hipLaunchKernelGGL(lse_combine_kernel<F16>, grid, dim3(256), 0, s, o1, lse1, o2, lse2, rows, D, gap, o, alpha);
-  else
-    return fail(VB_ERR_INVALID, "vb_lse_combine: unknown dtype");
-  return check_launch("lse_combine_kernel");
 }
