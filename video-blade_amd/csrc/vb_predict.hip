@@ -29,6 +29,7 @@ struct PredParams {
   const void* q; const void* k;
   int64_t qs[3], ks[3];
   uint8_t* q_s; uint8_t* k_s;   // sampled rows [B,H,nb*32,D] contiguous (workspace)
+  uint16_t* rbuf;               // R [B,H,nb(q-block),nb(key block),32 rows] storage bits (workspace)
   const int32_t* rows;
   const int32_t* q_off; const int32_t* k_off;
   int B, H, L, D, block, nb;
@@ -192,15 +193,14 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   constexpr int kRowsPerInst = 1024 / kRowB;          // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerWave = kTileBytes / 1024 / kPWaves;
   constexpr int kBufs = 4;                            // tiles t (read), t+1, t+2 in flight, t+3 issued
-  // LDS: R [4 waves][32 rows][rstride] storage dtype | m [4][32] f32 | K tiles x4 (after the main
-  //      loop: per-wave row scratch)
+  // LDS: m [4][32] f32 | K tiles x4 (after the main loop: per-wave row scratch). The per-row
+  // block maxima R go to a global scratch in [key block][32 rows] order (as the Triton kernel keeps
+  // R in HBM): a tile's two columns are one contiguous 128-byte store, and the LDS stays small
+  // enough for 3 workgroups per CU at any nb.
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nb = p.nb;
-  const int rstride = (nb + 7) & ~7;
-  typename T::raw* R = reinterpret_cast<typename T::raw*>(smem);
-  const int r_bytes = (kPWaves * 32 * rstride * 2 + 15) & ~15;
-  float* mrow_s = reinterpret_cast<float*>(smem + r_bytes);
-  uint8_t* ktile = smem + r_bytes + kPWaves * 32 * 4;
+  float* mrow_s = reinterpret_cast<float*>(smem);
+  uint8_t* ktile = smem + kPWaves * 32 * 4;
   float* rowbuf = reinterpret_cast<float*>(ktile);  // [4][2][kMaxNb + 4], reused after the loop
 
   const int lane = threadIdx.x & 63;
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     const int sw = (D == 64) ? ((l32 >> 1) & 7) : (l32 & 15);
     k_lane[ks] = l32 * kRowB + 16 * ((2 * ks + half) ^ sw);
   }
-  typename T::raw* Rrow = R + (wave * 32 + l32) * rstride;
+  uint16_t* Rq = p.rbuf + ((int64_t)bh * nb + (wave_active ? qb : 0)) * nb * 32;   // this q-block
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     const int j = 2 * t + half;
     const bool second = 2 * t + 1 < nb;
     m = fmaxf(m, second ? fmaxf(mx[0], mx[1]) : mx[0]);
-    if (j < nb) Rrow[j] = T::from_f32(half ? mx[1] : mx[0]);
+    if (j < nb && wave_active) Rq[j * 32 + l32] = (uint16_t)storage_bits<T>(half ? mx[1] : mx[0]);
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
     body(t0, std::integral_constant<int, 0>{});
@@ -312,12 +312,13 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   float* val = rowbuf + wave * 2 * (kMaxNb + 4);
   uint32_t* keys = reinterpret_cast<uint32_t*>(val + kMaxNb + 4);
   const float* mw = mrow_s + wave * 32;
-  const typename T::raw* Rw = R + wave * 32 * rstride;
+  // this wave's R columns were stored by its own lanes: wait for them and drop any stale L1 line
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   float part = 0.f;
   for (int j = lane; j < nb; j += 64) {
     float cm = -INFINITY;
 #pragma unroll 8
-    for (int r = 0; r < 32; ++r) cm = fmaxf(cm, T::to_f32(Rw[r * rstride + j]) - mw[r]);
+    for (int r = 0; r < 32; ++r) cm = fmaxf(cm, T::bits_to_f32(Rq[j * 32 + r]) - mw[r]);
     cm = round_to<T>(exp2_fast(cm));
     val[j] = cm;
     part += cm;
@@ -359,16 +360,20 @@ __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int ro
 }
 
 static size_t predict_smem_bytes(int nb, int D) {
-  const int rstride = (nb + 7) & ~7;
-  const size_t r_bytes = ((size_t)kPWaves * 32 * rstride * 2 + 15) & ~size_t(15);
+  (void)nb;
   const size_t tiles = 4 * (size_t)kKeysPerTile * D * 2;
   const size_t scratch = (size_t)kPWaves * 2 * (kMaxNb + 4) * 4;
-  return r_bytes + kPWaves * 32 * 4 + (tiles > scratch ? tiles : scratch);
+  return kPWaves * 32 * 4 + (tiles > scratch ? tiles : scratch);
 }
 
-static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
+// workspace: sampled q rows | sampled k rows | R
+static uint64_t predict_rows_bytes(int B, int H, int L, int D) {
   const int nb = (L + 127) / 128;
-  return 2 * ((uint64_t)B * H * nb * 32 * D * 2);
+  return (uint64_t)B * H * nb * 32 * D * 2;
+}
+static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
+  const uint64_t nb = (L + 127) / 128;
+  return 2 * predict_rows_bytes(B, H, L, D) + (uint64_t)B * H * nb * nb * 32 * 2;
 }
 
 template <int D, class T>
@@ -408,7 +413,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   const uint64_t ws = predict_ws_bytes(a->B, a->H, a->L, a->D);
   if (!a->workspace || a->workspace_bytes < ws || (reinterpret_cast<uintptr_t>(a->workspace) & 15))
     return fail(VB_ERR_INVALID, "vb_mask_predict: workspace missing or smaller than vb_mask_predict_workspace_size()");
-  if (ws / 2 / a->B / a->H >= (uint64_t(1) << 31)) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: sampled stream too large");
+  const uint64_t rows_b = predict_rows_bytes(a->B, a->H, a->L, a->D);
+  if (rows_b / a->B / a->H >= (uint64_t(1) << 31)) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: sampled stream too large");
   for (int i = 0; i < 3; ++i)
     if ((a->q_stride[i] | a->k_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_mask_predict: strides must be multiples of 8");
   PredParams p{};
@@ -422,7 +428,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   p.min_keep = a->min_keep; p.max_keep = a->max_keep; p.force_tail = a->force_tail;
   p.po = a->po; p.mask = a->mask; p.count = a->mask_count;
   p.q_s = reinterpret_cast<uint8_t*>(a->workspace);
-  p.k_s = p.q_s + ws / 2;
+  p.k_s = p.q_s + rows_b;
+  p.rbuf = reinterpret_cast<uint16_t*>(p.k_s + rows_b);
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);
 #endif
