@@ -23,7 +23,10 @@ namespace vb {
 constexpr int kPThreads = 256;
 constexpr int kPWaves = 4;
 constexpr int kMaxNb = 320;        // sampled blocks per side (L <= 40960 at block 128)
-constexpr int kKeysPerTile = 64;   // two 32-key sampled blocks per LDS tile
+// keys per LDS tile: D=64 streams four 32-key sampled blocks per barrier (16 MFMAs per wave),
+// D=128 two (also 16 MFMAs); a 3-deep ring keeps the LDS at 48 KiB (3 workgroups per CU)
+template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
+template <int D> constexpr int kPBufs = 3;
 
 struct PredParams {
   const void* q; const void* k;
@@ -189,10 +192,11 @@ template <int D, class T>
 __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredParams p) {
   constexpr int KS = D / 16;
   constexpr int kRowB = D * 2;                        // bytes per key row
-  constexpr int kTileBytes = kKeysPerTile * kRowB;
+  constexpr int kKT = kKeysPerTile<D> / 32;          // sampled key blocks per tile
+  constexpr int kTileBytes = kKeysPerTile<D> * kRowB;
   constexpr int kRowsPerInst = 1024 / kRowB;          // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerWave = kTileBytes / 1024 / kPWaves;
-  constexpr int kBufs = 4;                            // tiles t (read), t+1, t+2 in flight, t+3 issued
+  constexpr int kBufs = kPBufs<D>;                    // tile t read, the younger ones in flight
   // LDS: m [4][32] f32 | K tiles x4 (after the main loop: per-wave row scratch). The per-row
   // block maxima R go to a global scratch in [key block][32 rows] order (as the Triton kernel keeps
   // R in HBM): a tile's two columns are one contiguous 128-byte store, and the LDS stays small
@@ -228,7 +232,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   }
   // K tiles by LDS-DMA from the contiguous sampled stream: a buffer descriptor per (b,h), each
   // lane's fixed (row, swizzled chunk) as voffset, the tile's first row as soffset. Rows past the
-  // stream (odd nb: the last tile's second block) read as zeros and are never used.
+  // stream (a partial last tile) read as zeros and are never used.
   const srd_t ksrd = make_srd(p.k_s + bh * slice, (int)slice);
   int voff[kInstPerWave];
 #pragma unroll
@@ -241,7 +245,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   float m = -INFINITY;
   __syncthreads();   // all plain global loads retired before the DMA pipeline
 
-  const int ntiles = (VB_DIAG && (p.dbg & 2)) ? 0 : (nb + 1) / 2;
+  const int ntiles = (VB_DIAG && (p.dbg & 2)) ? 0 : (nb + kKT - 1) / kKT;
   // K tile t by LDS-DMA (global_load_lds_dwordx4): the LDS image is written linearly (1 KiB per
   // wave-instruction), so the 16-byte-chunk XOR swizzle of the image is applied to each lane's
   // SOURCE address: LDS slot `sl` of row r holds chunk sl ^ sw(r).
@@ -272,9 +276,9 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     __builtin_amdgcn_s_barrier();
     if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
     const uint8_t* kl = ktile + u * kTileBytes;
-    float mx[2];
+    float mx[kKT];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < kKT; ++kt) {
       typename T::vec8 kf[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -290,19 +294,26 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
       x = fmaxf(x, sc[15]);
       mx[kt] = max_xor32(x) * p.c;                   // tl.max(qk, 1) * qk_scale
     }
-    // half 0 stores block 2t, half 1 block 2t+1 (both halves hold both row maxima)
-    const int j = 2 * t + half;
-    const bool second = 2 * t + 1 < nb;
-    m = fmaxf(m, second ? fmaxf(mx[0], mx[1]) : mx[0]);
-    if (j < nb && wave_active) Rq[j * 32 + l32] = (uint16_t)storage_bits<T>(half ? mx[1] : mx[0]);
+    // every lane holds all kKT row maxima of its row; each store instruction writes two columns
+    // (half 0 the even, half 1 the odd one) as 128 contiguous bytes
+    const int j0 = kKT * t;
+#pragma unroll
+    for (int kt = 0; kt < kKT; ++kt)
+      if (j0 + kt < nb) m = fmaxf(m, mx[kt]);
+#pragma unroll
+    for (int pr = 0; pr < kKT / 2; ++pr) {
+      const int j = j0 + 2 * pr + half;
+      if (j < nb && wave_active) Rq[j * 32 + l32] = (uint16_t)storage_bits<T>(half ? mx[2 * pr + 1] : mx[2 * pr]);
+    }
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
     body(t0, std::integral_constant<int, 0>{});
     if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
     if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
-    if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
+    if constexpr (kBufs > 3)
+      if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
   }
-  static_assert(kBufs == 4, "the loop body is instantiated once per ring slot");
+  static_assert(kBufs == 3 || kBufs == 4, "the loop body is instantiated once per ring slot");
   if (half == 0) mrow_s[wave * 32 + l32] = m;
   __syncthreads();
   if (!wave_active || (VB_DIAG && (p.dbg & 1))) return;
@@ -361,7 +372,8 @@ __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int ro
 
 static size_t predict_smem_bytes(int nb, int D) {
   (void)nb;
-  const size_t tiles = 4 * (size_t)kKeysPerTile * D * 2;
+  const size_t tiles = D == 64 ? (size_t)kPBufs<64> * kKeysPerTile<64> * 64 * 2
+                               : (size_t)kPBufs<128> * kKeysPerTile<128> * 128 * 2;
   const size_t scratch = (size_t)kPWaves * 2 * (kMaxNb + 4) * 4;
   return kPWaves * 32 * 4 + (tiles > scratch ? tiles : scratch);
 }
