@@ -133,6 +133,13 @@ typedef struct vb_predict_args {
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);
 
+/* random_sample_tokens' index draw (cogvideo_blocksparseattn.py:45-46): the caller draws the
+ * uniforms (torch.rand(B,H,1,block), q first then k, so the RNG stream is the reference's); this
+ * replaces the two topk(num_keep) calls: rand_q/rand_k fp32 [rows, n] -> q_off/k_off int32
+ * [rows, keep], indices of the `keep` largest values in descending order (ties: lower index first). */
+int vb_sample_offsets(const float* rand_q, const float* rand_k, int rows, int n, int keep,
+                      int32_t* q_off, int32_t* k_off, void* stream);
+
 /* Energy rule alone on given scores (transfer_attn_to_mask, mode="energy"):
  * po [B,H,nr,nc] contiguous storage dtype -> mask [B,H,nr,nc]. */
 int vb_energy_mask(const void* po, int B, int H, int nr, int nc, float energy_threshold,

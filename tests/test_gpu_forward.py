@@ -287,3 +287,21 @@ def test_forward_is_bitwise_deterministic_at_full_size(variant, H, D):
                 for _ in range(4)]
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
+
+
+def test_sample_offsets_match_torch_topk_and_rng_order():
+    """vb_sample_offsets == torch.topk(rand, 32).indices (the reference's random_sample_tokens,
+    :45-46), and the module draws q then k from the same generator stream as the reference."""
+    from vblade import attention, ops
+    g = torch.Generator(device=DEV).manual_seed(123)
+    rq = torch.rand(2, 5, 1, 128, device=DEV, generator=g)
+    rk = torch.rand(2, 5, 1, 128, device=DEV, generator=g)
+    oq, ok = ops.sample_offsets(rq, rk, 32)
+    assert torch.equal(oq.long(), torch.topk(rq, 32, dim=3).indices)
+    assert torch.equal(ok.long(), torch.topk(rk, 32, dim=3).indices)
+    g1 = torch.Generator(device=DEV).manual_seed(7)
+    q_off, k_off = attention.draw_sample_offsets_qk(2, 5, DEV, generator=g1)
+    g2 = torch.Generator(device=DEV).manual_seed(7)
+    ref_q = attention.draw_sample_offsets(2, 5, DEV, generator=g2)
+    ref_k = attention.draw_sample_offsets(2, 5, DEV, generator=g2)
+    assert torch.equal(q_off, ref_q) and torch.equal(k_off, ref_k)

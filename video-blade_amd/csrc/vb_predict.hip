@@ -350,6 +350,28 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   if (p.count && lane == 0) atomicAdd(p.count, (unsigned long long)kept);
 }
 
+// random_sample_tokens' topk (cogvideo_blocksparseattn.py:45-46): for every row of `n` uniform draws,
+// the indices of the `keep` largest values in descending order of value (ties -> lower index
+// first). One wave per row; blockIdx.y selects the q or the k draws.
+__global__ void __launch_bounds__(256) topk_offsets_kernel(const float* rq, const float* rk, int rows, int n,
+                                                           int keep, int32_t* oq, int32_t* ok) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const float* r = (blockIdx.y ? rk : rq) + (int64_t)row * n;
+  int32_t* o = (blockIdx.y ? ok : oq) + (int64_t)row * keep;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const float v = i < n ? r[i] : 0.f;
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+      const float w = r[j];   // wave-uniform address: one broadcast load per step
+      rank += (w > v || (w == v && j < i)) ? 1 : 0;
+    }
+    if (i < n && rank < keep) o[rank] = i;
+  }
+}
+
 template <class T>
 __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int rows_total, int nc, float thr,
                                                           int min_keep, int max_keep, int force_tail, int nr,
@@ -478,4 +500,14 @@ extern "C" int vb_energy_mask(const void* po, int B, int H, int nr, int nc, floa
   else
     return fail(VB_ERR_INVALID, "vb_energy_mask: unknown dtype");
   return check_launch("energy_mask_kernel");
+}
+
+extern "C" int vb_sample_offsets(const float* rand_q, const float* rand_k, int rows, int n, int keep,
+                                 int32_t* q_off, int32_t* k_off, void* stream) {
+  using namespace vb;
+  if (!rand_q || !rand_k || !q_off || !k_off) return fail(VB_ERR_INVALID, "vb_sample_offsets: null argument");
+  if (rows <= 0 || n <= 0 || keep <= 0 || keep > n) return fail(VB_ERR_INVALID, "vb_sample_offsets: bad sizes");
+  hipLaunchKernelGGL(topk_offsets_kernel, dim3((rows + 3) / 4, 2), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     rand_q, rand_k, rows, n, keep, q_off, k_off);
+  return check_launch("topk_offsets_kernel");
 }

@@ -95,6 +95,7 @@ SIGNATURES = {
     "vb_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnArgs), _vp]),
     "vb_mask_predict_workspace_size": (ctypes.c_uint64, [ctypes.POINTER(PredictArgs)]),
     "vb_mask_predict": (ctypes.c_int, [ctypes.POINTER(PredictArgs), _vp]),
+    "vb_sample_offsets": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
     "vb_energy_mask": (ctypes.c_int, [
         _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),

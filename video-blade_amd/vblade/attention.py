@@ -58,6 +58,17 @@ def draw_sample_offsets(B: int, H: int, device, block: int = 128, num_keep: int 
     return torch.topk(r, num_keep, dim=3).indices[:, :, 0, :].to(torch.int32)
 
 
+def draw_sample_offsets_qk(B: int, H: int, device, block: int = 128, num_keep: int = 32,
+                           generator: Optional[torch.Generator] = None):
+    """The q and k draws of efficient_attn_with_pooling (:77-78): two torch.rand calls in the
+    reference's order (the same RNG stream), the two topk selections in one HIP launch
+    (vb_sample_offsets; same indices as torch.topk for distinct values)."""
+    rq = torch.rand(B, H, 1, block, device=device, generator=generator)
+    rk = torch.rand(B, H, 1, block, device=device, generator=generator)
+    q_off, k_off = ops.sample_offsets(rq, rk, num_keep)
+    return q_off[:, :, 0, :], k_off[:, :, 0, :]
+
+
 class GilbertRearranger(nn.Module):
     """Index maps of the Gilbert reorder (cogvideo_blocksparseattn.py:110-161; wanx :102-159).
 
@@ -176,6 +187,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
     def predict_mask(self, q, k, q_off=None, k_off=None, count=None):
         """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores."""
         B, H, L, D = q.shape
+        if q_off is None and k_off is None:
+            q_off, k_off = draw_sample_offsets_qk(B, H, q.device, self.block, self.num_keep)
         if q_off is None:
             q_off = draw_sample_offsets(B, H, q.device)
         if k_off is None:

@@ -311,6 +311,22 @@ def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_ke
     return po, mask
 
 
+def sample_offsets(rand_q, rand_k, keep: int = 32):
+    """vb_sample_offsets: topk(keep) indices (descending value, ties lower index first) of each
+    row of the uniform draws rand_q/rand_k [..., n] -> int32 [..., keep] (q, k)."""
+    dev = _require_gpu(rand_q, rand_k)
+    rand_q, rand_k = rand_q.float().contiguous(), rand_k.float().contiguous()
+    n = rand_q.shape[-1]
+    rows = rand_q.numel() // n
+    shape = tuple(rand_q.shape[:-1]) + (keep,)
+    oq = torch.empty(shape, device=dev, dtype=torch.int32)
+    ok = torch.empty(shape, device=dev, dtype=torch.int32)
+    check(_lib.load().vb_sample_offsets(rand_q.data_ptr(), rand_k.data_ptr(), rows, n, keep,
+                                        oq.data_ptr(), ok.data_ptr(), _stream(dev)),
+          "vb_sample_offsets")
+    return oq, ok
+
+
 def energy_mask(po, *, energy_threshold=0.95, min_keep=1, max_keep=1, force_tail=0, mask_count=None):
     """vb_energy_mask on scores po [B,H,nr,nc] (bf16/fp16) -> uint8 mask."""
     dev = _require_gpu(po)
