@@ -47,6 +47,12 @@ struct FwdParams {
 #ifndef VB_DIAG
 #define VB_DIAG 0
 #endif
+#ifndef VB_VPRE64
+#define VB_VPRE64 4   // V^T k-steps prefetched before the softmax (D=64)
+#endif
+#ifndef VB_MFMA_ROWSUM
+#define VB_MFMA_ROWSUM 0
+#endif
 #ifndef VB_FWD_WAVES_D64
 #define VB_FWD_WAVES_D64 3  // waves per SIMD the D=64 kernel is register-budgeted for
 #endif
@@ -121,6 +127,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
   const int half = lane >> 5;
   const int l32 = lane & 31;
 
@@ -314,6 +321,16 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
   float m = -INFINITY;  // running max (exp2 domain) of this lane's query row
   float l = 0.f;        // running partial row sum (this half's keys)
+#if VB_MFMA_ROWSUM
+  // Row sums on the matrix core (D=64 is VALU-bound): lsum += ones . P^T, every register of the
+  // accumulator = the lane's full row sum of the bf16 P that also feeds O (no VALU adds).
+  f32x16 lsum;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lsum[r] = 0.f;
+  typename T::vec8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = T::from_f32(1.0f);
+#endif
 
   const int vrow = 4 * half + (lane & 15) / 4;
   const int vcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
@@ -351,7 +368,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     }
     // V^T fragments (ds_read_b64_tr_b16) for the first VPRE k-steps, issued before the softmax
     // VALU so they land while it runs; the rest are fetched one k-step ahead inside the PV loop.
-    constexpr int VPRE = (D == 64) ? 4 : 2;
+    constexpr int VPRE = (D == 64 && !VB_MFMA_ROWSUM) ? VB_VPRE64 : 2;
     s16x4 vlo[4][DT], vhi[4][DT];
     auto read_v = [&](int kk) __attribute__((always_inline)) {
       const int row0 = (kk >> 1) * 32 + 16 * (kk & 1);   // + vrow (in v_lane)
@@ -400,6 +417,10 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       const float alpha = exp2_fast(m - mn);
       m = mn;
       l *= alpha;
+#if VB_MFMA_ROWSUM
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
+#endif
 #pragma unroll
       for (int i = 0; i < DT; ++i)
 #pragma unroll
@@ -416,6 +437,11 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
           s[kt][r] = e;
           ls += e;
         }
+    } else if (VB_MFMA_ROWSUM) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kt][r] = exp2_fast(fmaf(s[kt][r], p.c, nbias));
     } else {
       float lq[4] = {0.f, 0.f, 0.f, 0.f};   // four independent partial sums
 #pragma unroll
@@ -439,6 +465,9 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       const typename T::vec8 pf = pack8<T>(s[kk >> 1], 8 * (kk & 1));
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo[kk][dt], vhi[kk][dt]), pf, o[dt]);
+#if VB_MFMA_ROWSUM
+      lsum = T::mfma32(ones, pf, lsum);
+#endif
     }
     VB_STAMP(s3);
     VB_ACC(4, s3 - s2);
@@ -503,7 +532,11 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
 #endif
 
   // ---- epilogue -----------------------------------------------------------------------------------
+#if VB_MFMA_ROWSUM
+  const float lt = lsum[0];
+#else
   const float lt = add_xor32(l);
+#endif
   const float inv = (lt > 0.f) ? 1.0f / lt : 0.f;
   // streaming heads (unsupported) are flagged with NaN outputs written as bit patterns: this
   // translation unit is compiled with -fno-honor-nans, so no float arithmetic may produce them
