@@ -65,6 +65,8 @@ struct BwdParams {
   void* dq; int64_t dqs[3]; const int32_t* q_rows;
   void* dk; void* dv; int64_t dks[3], dvs[3]; const int32_t* kv_rows;
   float* dkp; float* dvp;  // [B,H,Lkp,D] fp32 pooled-key grads
+  int psplit;              // pooled-key workgroups split the q-blocks in psplit ranges...
+  float* dkp_part; float* dvp_part;  // ...into [psplit][B,H,Lkp,D] partials (== dkp/dvp if 1)
   int gap;
   int B, H, Lq, Lk, nbq, nbk, nbkp;
   float c;      // scale * log2(e)
@@ -173,8 +175,10 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 
   const int BH = p.B * p.H;
   const int nkb = kPooled ? p.nbkp : p.nbk;
-  // pooled-key blocks see every q-block (long workgroups): plain order; main blocks XCD-contiguous
-  const int lin = kPooled ? (int)blockIdx.x : xcd_linear(blockIdx.x, nkb * BH);
+  // pooled-key blocks see every q-block: their work is split into psplit q-block ranges (split
+  // innermost, so a key block's workgroups run together); main blocks XCD-contiguous
+  const int split = kPooled ? (int)blockIdx.x % p.psplit : 0;
+  const int lin = kPooled ? (int)blockIdx.x / p.psplit : xcd_linear(blockIdx.x, nkb * BH);
   const int bh = lin / nkb;
   const int kblk = lin % nkb;
   const int b = bh / p.H, h = bh % p.H;
@@ -196,11 +200,13 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
     const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
     if (mh) mcol = mh + kblk;
   }
+  const int qlo = kPooled ? split * nbq / p.psplit : 0;
+  const int qhi = kPooled ? (split + 1) * nbq / p.psplit : nbq;
   if (threadIdx.x < 64) {
     int n = 0;
-    for (int i0 = 0; i0 < nbq; i0 += 64) {
+    for (int i0 = qlo; i0 < qhi; i0 += 64) {
       const int i = i0 + lane;
-      const bool keep = (i < nbq) && (mcol == nullptr || mcol[(int64_t)i * p.ms[2]] != 0);
+      const bool keep = (i < qhi) && (mcol == nullptr || mcol[(int64_t)i * p.ms[2]] != 0);
       const unsigned long long bal = __ballot(keep);
       if (keep) {
         const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
@@ -320,10 +326,10 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
         const int rr = 32 * u + 16 * sb + trr;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          s16x4 dol = lds_tr4(dot, dual_off_col<D>(rr, 32 * dt + trc));
-          s16x4 doh = lds_tr4(dot, dual_off_col<D>(rr + 8, 32 * dt + trc));
-          s16x4 ql = lds_tr4(qt, dual_off_col<D>(rr, 32 * dt + trc));
-          s16x4 qh = lds_tr4(qt, dual_off_col<D>(rr + 8, 32 * dt + trc));
+          s16x4 dol = lds_tr4_asm_at(dot, dual_off_col<D>(rr, 32 * dt + trc));
+          s16x4 doh = lds_tr4_asm_at(dot, dual_off_col<D>(rr + 8, 32 * dt + trc));
+          s16x4 ql = lds_tr4_asm_at(qt, dual_off_col<D>(rr, 32 * dt + trc));
+          s16x4 qh = lds_tr4_asm_at(qt, dual_off_col<D>(rr + 8, 32 * dt + trc));
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(dol), "+v"(doh), "+v"(ql), "+v"(qh));
           dv[dt] = T::mfma32(join8<T>(dol, doh), pp, dv[dt]);
           dk[dt] = T::mfma32(join8<T>(ql, qh), pd, dk[dt]);
@@ -337,8 +343,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
   if (!kvalid) return;
   const float nanf_ = __builtin_nanf("");
   if (kPooled) {
-    float* dkr = p.dkp + ((int64_t)bh * p.Lkp + key) * D;
-    float* dvr = p.dvp + ((int64_t)bh * p.Lkp + key) * D;
+    const int64_t po = ((int64_t)split * BH + bh) * p.Lkp + key;
+    float* dkr = p.dkp_part + po * D;
+    float* dvr = p.dvp_part + po * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -600,8 +607,8 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
         const int rr = kt * 32 + 16 * sb + trr;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          s16x4 lo = lds_tr4(kt_, dual_off_col<D>(rr, 32 * dt + trc));
-          s16x4 hi = lds_tr4(kt_, dual_off_col<D>(rr + 8, 32 * dt + trc));
+          s16x4 lo = lds_tr4_asm_at(kt_, dual_off_col<D>(rr, 32 * dt + trc));
+          s16x4 hi = lds_tr4_asm_at(kt_, dual_off_col<D>(rr + 8, 32 * dt + trc));
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi));
           dq[dt] = T::mfma32(join8<T>(lo, hi), pd, dq[dt]);
         }
@@ -626,6 +633,21 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
     }
 }
 
+// sum of the pooled-key gradient partials: dkp = sum_s part[s] (fixed order: deterministic)
+__global__ void __launch_bounds__(256) pool_grad_reduce_kernel(const float* pk, const float* pv, int64_t n4, int nsplit,
+                                                               float* dk, float* dv) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  f32x4 a = reinterpret_cast<const f32x4*>(pk)[i];
+  f32x4 c = reinterpret_cast<const f32x4*>(pv)[i];
+  for (int s = 1; s < nsplit; ++s) {
+    a += reinterpret_cast<const f32x4*>(pk)[s * n4 + i];
+    c += reinterpret_cast<const f32x4*>(pv)[s * n4 + i];
+  }
+  reinterpret_cast<f32x4*>(dk)[i] = a;
+  reinterpret_cast<f32x4*>(dv)[i] = c;
+}
+
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
@@ -641,8 +663,14 @@ template <int D, class T>
 static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
   const int BH = p.B * p.H;
   if (pool && p.dkp) {
-    hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true>), dim3(p.nbkp * BH), dim3(bwd::kThreads), 0, s, p);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true>), dim3(p.nbkp * BH * p.psplit), dim3(bwd::kThreads), 0, s, p);
     if (int rc = check_launch("bwd_dkdv_kernel<pooled>")) return rc;
+    if (p.psplit > 1) {
+      const int64_t n4 = (int64_t)BH * p.Lkp * D / 4;
+      hipLaunchKernelGGL(pool_grad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, p.dkp_part,
+                         p.dvp_part, n4, p.psplit, p.dkp, p.dvp);
+      if (int rc = check_launch("pool_grad_reduce_kernel")) return rc;
+    }
   }
   if (p.k) {
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, false>), dim3(p.nbk * BH), dim3(bwd::kThreads), 0, s, p);
@@ -667,8 +695,17 @@ static int dispatch_bwd(const PrepParams& pp, const BwdParams& p, int D, int dty
 }
 
 struct WsLayout {
-  uint64_t stats, q_r, do_r, dkp, dvp, total;
+  uint64_t stats, q_r, do_r, dkp, dvp, dkp_part, dvp_part, total;
+  int psplit;
 };
+// pooled-key q-range split: aim at ~3k workgroups for the pooled dK/dV pass
+static int pool_split(int B, int H, int Lq, int Lkp) {
+  if (Lkp <= 0) return 1;
+  const int nbkp = (Lkp + 127) / 128, nbq = (Lq + 127) / 128;
+  const int wg = nbkp * B * H;
+  int s = (3072 + wg / 2) / wg;
+  return s < 1 ? 1 : (s > nbq ? nbq : s);
+}
 static WsLayout ws_layout(int B, int H, int Lq, int D, bool copies, int Lkp) {
   auto up = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   WsLayout w{};
@@ -680,10 +717,16 @@ static WsLayout ws_layout(int B, int H, int Lq, int D, bool copies, int Lkp) {
     w.q_r = off; off = up(off + (uint64_t)B * H * Lq * D * 2);
     w.do_r = off; off = up(off + (uint64_t)B * H * Lq * D * 2);
   }
-  w.dkp = w.dvp = 0;
+  w.dkp = w.dvp = w.dkp_part = w.dvp_part = 0;
+  w.psplit = pool_split(B, H, Lq, Lkp);
   if (Lkp > 0) {
     w.dkp = off; off = up(off + (uint64_t)B * H * Lkp * D * 4);
     w.dvp = off; off = up(off + (uint64_t)B * H * Lkp * D * 4);
+    w.dkp_part = w.dkp; w.dvp_part = w.dvp;
+    if (w.psplit > 1) {
+      w.dkp_part = off; off = up(off + (uint64_t)w.psplit * B * H * Lkp * D * 4);
+      w.dvp_part = off; off = up(off + (uint64_t)w.psplit * B * H * Lkp * D * 4);
+    }
   }
   w.total = off;
   return w;
@@ -767,7 +810,12 @@ extern "C" int vb_attn_bwd(const vb_attn_bwd_args* a, void* stream) {
   p.stats = pp.stats; p.ntile = pp.ntile;
   p.dq = a->dq; p.q_rows = a->q_rows;
   p.dk = a->dk; p.dv = a->dv; p.kv_rows = a->kv_rows;
-  if (pool) { p.dkp = reinterpret_cast<float*>(ws + w.dkp); p.dvp = reinterpret_cast<float*>(ws + w.dvp); }
+  p.psplit = 1;
+  if (pool) {
+    p.dkp = reinterpret_cast<float*>(ws + w.dkp); p.dvp = reinterpret_cast<float*>(ws + w.dvp);
+    p.psplit = w.psplit;
+    p.dkp_part = reinterpret_cast<float*>(ws + w.dkp_part); p.dvp_part = reinterpret_cast<float*>(ws + w.dvp_part);
+  }
   p.gap = pool ? a->pool_gap : 1;
   p.B = a->B; p.H = a->H; p.Lq = a->Lq; p.Lk = a->Lk; p.nbq = nbq; p.nbk = nbk;
   p.nbkp = pool ? (a->Lkp + 127) / 128 : 0;
@@ -834,6 +882,7 @@ extern "C" int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, c
   p.stats = pp.stats; p.ntile = pp.ntile;
   p.dq = dq; p.dk = dk; p.dv = dv;
   p.gap = 1;
+  p.psplit = 1;
   p.B = batch; p.H = num_heads; p.Lq = max_seqlen_q; p.Lk = max_seqlen_k; p.nbq = nbq; p.nbk = nbk;
   p.scale = softmax_scale > 0.f ? softmax_scale : (float)(1.0 / sqrt((double)head_dim));
   p.c = p.scale * kLog2e;

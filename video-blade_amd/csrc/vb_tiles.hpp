@@ -37,6 +37,13 @@ __device__ __forceinline__ s16x4 lds_tr4_imm(uint32_t lane_addr, int imm) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       reinterpret_cast<__attribute__((address_space(3))) s16x4*>(static_cast<uintptr_t>(lane_addr + imm)));
 }
+__device__ __forceinline__ s16x4 lds_tr4_asm_at(const uint8_t* base, int off) {
+  const uint32_t a = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)(base + off)));
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
 __device__ __forceinline__ s16x4 lds_tr4_asm(uint32_t lane_addr, int imm) {
   s16x4 r;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lane_addr), "i"(imm));
