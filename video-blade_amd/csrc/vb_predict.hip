@@ -168,13 +168,12 @@ __device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int n
 // read at the caller's row rows[pos]. The predictor then streams K by plain LDS-DMA.
 template <class T>
 __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
+  // one thread per sampled row: the two index loads once, then D/8 independent 16-byte copies
   const int CH = p.D / 8;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nrow = (int64_t)p.nb * 32;
-  if (idx >= (int64_t)p.B * p.H * nrow * CH) return;
+  if (r >= (int64_t)p.B * p.H * nrow) return;
   const bool isk = blockIdx.y != 0;
-  const int ch = idx % CH;
-  const int64_t r = idx / CH;
   const int jt = r % nrow;
   const int bh = r / nrow;
   const int b = bh / p.H, h = bh % p.H;
@@ -182,10 +181,22 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
   int pos = min((jt >> 5) * p.block + off[jt & 31], p.L - 1);
   if (p.rows) pos = p.rows[pos];
   const int64_t* st = isk ? p.ks : p.qs;
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(isk ? p.k : p.q) +
-                       2 * (b * st[0] + h * st[1] + (int64_t)pos * st[2]) + ch * 16;
-  uint8_t* dst = (isk ? p.k_s : p.q_s) + (r * p.D + ch * 8) * 2;
-  *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+  const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(isk ? p.k : p.q) +
+                                                    2 * (b * st[0] + h * st[1] + (int64_t)pos * st[2]));
+  u32x4* dst = reinterpret_cast<u32x4*>((isk ? p.k_s : p.q_s) + r * p.D * 2);
+  if (CH == 8) {
+    u32x4 x[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) x[c] = src[c];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) dst[c] = x[c];
+  } else {
+    u32x4 x[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[c] = src[c];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dst[c] = x[c];
+  }
 }
 
 template <int D, class T>
@@ -355,17 +366,22 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
 // first). One wave per row; blockIdx.y selects the q or the k draws.
 __global__ void __launch_bounds__(256) topk_offsets_kernel(const float* rq, const float* rk, int rows, int n,
                                                            int keep, int32_t* oq, int32_t* ok) {
+  __shared__ float buf[4][256];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
-  if (row >= rows) return;
+  if (row >= rows || n > 256) return;
   const float* r = (blockIdx.y ? rk : rq) + (int64_t)row * n;
   int32_t* o = (blockIdx.y ? ok : oq) + (int64_t)row * keep;
+  float* sv = buf[wave];
+  for (int i = lane; i < n; i += 64) sv[i] = r[i];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
   for (int i0 = 0; i0 < n; i0 += 64) {
     const int i = i0 + lane;
-    const float v = i < n ? r[i] : 0.f;
+    const float v = i < n ? sv[i] : 0.f;
     int rank = 0;
     for (int j = 0; j < n; ++j) {
-      const float w = r[j];   // wave-uniform address: one broadcast load per step
+      const float w = sv[j];   // LDS broadcast
       rank += (w > v || (w == v && j < i)) ? 1 : 0;
     }
     if (i < n && rank < keep) o[rank] = i;
@@ -417,7 +433,7 @@ static int launch_predict(const PredParams& p, hipStream_t stream) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)smem) != hipSuccess)
     return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
-  const int64_t gthreads = (int64_t)p.B * p.H * p.nb * 32 * (D / 8);
+  const int64_t gthreads = (int64_t)p.B * p.H * p.nb * 32;
   hipLaunchKernelGGL(sample_rows_kernel<T>, dim3((unsigned)((gthreads + 255) / 256), 2), dim3(256), 0, stream, p);
   if (int rc = check_launch("sample_rows_kernel")) return rc;
   const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H);
@@ -507,6 +523,7 @@ extern "C" int vb_sample_offsets(const float* rand_q, const float* rand_k, int r
   using namespace vb;
   if (!rand_q || !rand_k || !q_off || !k_off) return fail(VB_ERR_INVALID, "vb_sample_offsets: null argument");
   if (rows <= 0 || n <= 0 || keep <= 0 || keep > n) return fail(VB_ERR_INVALID, "vb_sample_offsets: bad sizes");
+  if (n > 256) return fail(VB_ERR_UNSUPPORTED, "vb_sample_offsets: at most 256 draws per row");
   hipLaunchKernelGGL(topk_offsets_kernel, dim3((rows + 3) / 4, 2), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      rand_q, rand_k, rows, n, keep, q_off, k_off);
   return check_launch("topk_offsets_kernel");
