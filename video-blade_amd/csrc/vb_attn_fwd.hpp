@@ -1,0 +1,73 @@
+// Shared definitions of the block-sparse attention forward kernel (vb_attn_fwd.hip).
+#pragma once
+#include "vb_tiles.hpp"
+
+namespace vb {
+
+struct FwdParams {
+  const void* q; const void* k; const void* v;
+  int64_t qs[3], ks[3], vs[3];
+  const int32_t* q_rows; const int32_t* kv_rows;
+  const int32_t* cu_q; const int32_t* cu_k;   // varlen row offsets (reference API), nullable
+  const int32_t* head_mask_type;              // reference API, nullable
+  int use_main;
+  const uint8_t* mask; int64_t ms[3];
+  const void* kp; const void* vp; int64_t kps[3], vps[3];
+  int Lkp; float pool_bias_l2;                 // bias in the exp2 domain (log2 gap)
+  void* out; int64_t os[3];
+  float* lse; int64_t lse_s[2];               // row stride 1
+  int B, H, Lq, Lk, nbq, nbk;
+  float c;                                    // softmax scale * log2(e)
+  int heavy_rows;                             // last q-block rows known to be dense (scheduling hint)
+  int dbg;                                    // diagnostic builds only (VB_DEBUG_ATTN)
+};
+
+#ifndef VB_DIAG
+#define VB_DIAG 0
+#endif
+#ifndef VB_VPRE64
+#define VB_VPRE64 4   // V^T k-steps prefetched before the softmax (D=64)
+#endif
+#ifndef VB_MFMA_ROWSUM
+#define VB_MFMA_ROWSUM 0
+#endif
+#ifndef VB_FWD_WAVES_D64
+#define VB_FWD_WAVES_D64 3  // waves per SIMD the D=64 kernel is register-budgeted for
+#endif
+
+constexpr int kThreads = 256;
+constexpr int kQBlk = 128;   // rows per workgroup (4 waves x 32)
+constexpr int kKT = 64;      // keys per LDS tile
+constexpr int kMaxBlocks = 1024;  // keys <= 131072
+#ifndef VB_RESCALE_SLACK
+#define VB_RESCALE_SLACK 4.0f
+#endif
+constexpr float kRescaleSlack = VB_RESCALE_SLACK;  // log2 units: P <= 16 between rescales
+
+// ---- LDS images --------------------------------------------------------------------------------
+// K: [64 rows][D] with 16-byte chunks XOR-swizzled so a ds_read_b128 column slice (32 rows, one
+//    chunk) hits 16 distinct bank slots per lane group (guide T2).
+template <int D>
+__device__ __forceinline__ int k_off(int row, int ch) {
+  constexpr int kRowBytes = D * 2;
+  const int sw = (D == 64) ? ((row >> 1) & 7) : (row & 15);
+  return row * kRowBytes + 16 * (ch ^ sw);
+}
+// V: [64 rows][D] row-major, 64-byte granules XOR-swizzled so the 4-row x 64-byte footprint of
+//    a half-wave's ds_read_b64_tr_b16 covers a full 256-byte bank row.
+template <int D>
+__device__ __forceinline__ int v_off_bytes(int row, int col) {
+  constexpr int kRowBytes = D * 2;
+  const int g = col >> 5;
+  const int sw = (D == 64) ? ((row >> 1) & 1) : (row & 3);
+  return row * kRowBytes + 64 * (g ^ sw) + (col & 31) * 2;
+}
+
+// Describes where tile t's keys come from.
+struct TileSrc {
+  int pooled;   // 0 = main (block-masked) keys, 1 = pooled keys
+  int kstart;   // first key (reordered index for main, pooled index otherwise)
+  int klen;     // valid keys in this tile (1..64)
+};
+
+}  // namespace vb
