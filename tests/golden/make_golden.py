@@ -14,6 +14,7 @@ Harness shims (test infrastructure only, none of them part of the product):
     masked-softmax restatement (oracle/bsa_oracle.py) is registered so the reference glue can be
     imported. Fixtures produced through it therefore pin the reference GLUE (reorder, padding,
     sampling, Triton pooled scores, energy mask, pooling, combine, un-reorder), not that op.
+  * the multi-level kernel wrapper's ``torch.cuda.device(...)`` context is a no-op (CPU tensors).
   * the CogVideoX GilbertRearranger hard-codes device='cuda' (cogvideo_blocksparseattn.py:127-128);
     it is built here through its own ``_gilbert3d_with_index`` with CPU index tensors.
 """
@@ -234,7 +235,111 @@ def gen_e2e(out, cog, wan):
     np.savez_compressed(os.path.join(out, "adaptive_e2e.npz"), **res)
 
 
+TRI = os.path.join(REF, "cogvideox/sample_evaluate")
+
+
+class _Ctx:
+    """Minimal autograd ctx for calling the reference kernel's _forward/_backward directly."""
+
+    def save_for_backward(self, *t):
+        self.saved_tensors = t
+
+
+def _import_multilevel():
+    """TRI/Triton/cogvideo_newattn.py and its kernel module (Triton interpreter on CPU)."""
+    sys.path.insert(0, TRI)
+    import importlib
+    kml = importlib.import_module("Triton.kernels.block_sparse_attn_kernel_with_backward_9_10")
+    kml.is_hip = lambda: False
+    # the kernel wrapper enters torch.cuda.device(q.device.index); with no GPU driver that raises
+    import contextlib
+    torch.cuda.device = lambda idx: contextlib.nullcontext()
+    apk = importlib.import_module("Triton.kernels.attn_pooling_kernel")
+    apk.is_hip = lambda: False
+    newattn = importlib.import_module("Triton.cogvideo_newattn")
+    sys.path.remove(TRI)
+    return newattn, kml
+
+
+def gen_multilevel(out):
+    """Multi-level path: level masks, KV pyramid, the Triton multi-level
+    kernel's forward (out, l, m) and backward (dq, dk, dv), and the whole
+    adaptive_block_sparse_attn of the VBench sampler module."""
+    import ml_oracle as ML
+    newattn, kml = _import_multilevel()
+    res = {}
+    g = torch.Generator().manual_seed(29)
+    # level masks on tie-heavy bf16 rows
+    for name, B, H, nb in [("m139", 1, 3, 139), ("m256", 1, 1, 256), ("m21", 2, 2, 21), ("m5", 1, 1, 5)]:
+        po = torch.rand(B, H, nb, nb, generator=g) ** 4
+        ties = (torch.rand(B, H, nb, nb, generator=g) < 0.15).float()
+        po = torch.where(torch.rand(B, H, nb, 1, generator=g) < 0.5, po, torch.maximum(po, ties))
+        po = (po / po.sum(-1, keepdim=True)).bfloat16()
+        res["lm_" + name + "_po"] = po.float().numpy()
+        res["lm_" + name + "_mask"] = newattn.transfer_attn_to_mask(po, newattn.mask_ratios).numpy()
+    # KV pyramid (pad_to_multiple + pooling, fp16 storage)
+    x = (torch.randn(1, 2, 300, 64, generator=g) * 2).half()
+    xp = kml.pad_to_multiple(x, 128)
+    x2 = kml.pooling(xp, 2)
+    x4 = kml.pooling(x2, 2)
+    x8 = kml.pooling(x4, 2)
+    res["pyr_x"] = x.float().numpy()
+    for nm, t in [("pad", xp), ("p2", x2), ("p4", x4), ("p8", x8)]:
+        res["pyr_" + nm] = t.float().numpy()
+    # the kernel itself: forward + backward on random level masks
+    cases = [("f32_d64", torch.float32, 1, 2, 300, 64), ("f16_d64", torch.float16, 1, 2, 300, 64),
+             ("f32_d128", torch.float32, 1, 1, 256, 128), ("f16_d128_b2", torch.float16, 2, 1, 200, 128)]
+    for name, dt, B, H, L, D in cases:
+        nb = (L + 127) // 128
+        q = torch.randn(B, H, L, D, generator=g).to(dt)
+        k = torch.randn(B, H, L, D, generator=g).to(dt)
+        v = torch.randn(B, H, L, D, generator=g).to(dt)
+        lv = torch.tensor([0, 1, 2, 4, 8], dtype=torch.int32)
+        mask = lv[torch.randint(0, 5, (B, H, nb, nb), generator=g)]
+        mask[..., -1] = 1          # every row attends somewhere
+        do = torch.randn(B, H, L, D, generator=g).to(dt)
+        ctx = _Ctx()
+        o = kml._forward(ctx, q.clone().requires_grad_(), k, v, mask, D ** -0.5, 128, 128, 128)
+        saved = ctx.saved_tensors
+        lsum, mmax = saved[12], saved[13]
+        dq, dk, dv, _, _ = kml._backward(ctx, do)
+        res.update({"k_" + name + "_q": q.float().numpy(), "k_" + name + "_k": k.float().numpy(),
+                    "k_" + name + "_v": v.float().numpy(), "k_" + name + "_mask": mask.numpy(),
+                    "k_" + name + "_do": do.float().numpy(), "k_" + name + "_out": o.detach().float().numpy(),
+                    "k_" + name + "_l": lsum.reshape(B, H, L).numpy(),
+                    "k_" + name + "_m": mmax.reshape(B, H, L).numpy(),
+                    "k_" + name + "_dq": dq.float().numpy(), "k_" + name + "_dk": dk.float().numpy(),
+                    "k_" + name + "_dv": dv.float().numpy(), "k_" + name + "_dtype": np.array(str(dt))})
+    # the whole adaptive_block_sparse_attn (sampler + Triton pooled scores + level mask + kernel)
+    for name, dt, H, L, D in [("e2e_f32", torch.float32, 1, 2600, 64), ("e2e_f16", torch.float16, 1, 2600, 64)]:
+        store = np.float16 if dt == torch.float16 else np.float32
+        cent = torch.randn(1, H, L // 16 + 1, D, generator=g).repeat_interleave(16, 2)[:, :, :L]
+        q = (torch.randn(1, H, L, D, generator=g) + 1.5 * cent).to(dt)
+        k = (torch.randn(1, H, L, D, generator=g) + 1.5 * cent).to(dt)
+        v = torch.randn(1, H, L, D, generator=g).to(dt)
+        torch.manual_seed(4321)
+        with torch.no_grad():
+            o, sp = newattn.adaptive_block_sparse_attn(q, k, v)
+        torch.manual_seed(4321)
+        qo = O.draw_sample_offsets(1, H)
+        ko = O.draw_sample_offsets(1, H)
+        torch.manual_seed(4321)
+        with torch.no_grad():
+            po = newattn.efficient_attn_with_pooling(q, k, v, block_size=128)
+        mask = newattn.transfer_attn_to_mask(po, newattn.mask_ratios)
+        res.update({name + "_q": q.float().numpy().astype(store), name + "_k": k.float().numpy().astype(store),
+                    name + "_v": v.float().numpy().astype(store), name + "_out": o.float().numpy().astype(store),
+                    name + "_qoff": qo.numpy().astype(np.int32), name + "_koff": ko.numpy().astype(np.int32),
+                    name + "_po": po.float().numpy(), name + "_mask": mask.numpy(),
+                    name + "_sparsity": np.array(sp), name + "_dtype": np.array(str(dt))})
+    assert abs(ML.density() - (1 - res["e2e_f32_sparsity"])) < 1e-12
+    np.savez_compressed(os.path.join(out, "multilevel.npz"), **res)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "multilevel":   # regenerate only multilevel.npz
+        gen_multilevel(HERE)
+        return
     _install_block_sparse_stub()
     cog, apk = _import_ref(COG_TRAIN, "cogvideo_blocksparseattn")
     wan, _ = _import_ref(WAN_TRAIN, "wanx_blocksparseattn")
@@ -243,6 +348,7 @@ def main():
     gen_energy_masks(HERE, cog, wan, apk)
     gen_sampling(HERE, cog)
     gen_e2e(HERE, cog, wan)
+    gen_multilevel(HERE)
     print("golden fixtures written to", HERE)
 
 
