@@ -220,6 +220,61 @@ int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, const void* 
                              void* dq, void* dk, void* dv, void* workspace, uint64_t workspace_bytes,
                              void* stream);
 
+/* ==========================================================================================
+ * Multi-level block-sparse attention: the VBench sampler's op (cogvideox/sample_evaluate/
+ * modify_cogvideo.py:9 -> Triton/cogvideo_newattn.py:210-234, kernel Triton/kernels/
+ * block_sparse_attn_kernel_with_backward_9_10.py). Every (query block i, key block j) pair has a
+ * level p in {0, 1, 2, 4, 8}: 0 skips the block, p > 0 attends to the block's 128/p keys of K/V
+ * mean-pooled by p, each with logit q.k*scale + ln p.
+ * ========================================================================================== */
+
+/* Rows of the KV pyramid of an L-row sequence: 15*Lpad/8 with Lpad = ceil(L/128)*128. */
+int vb_kv_pyramid_rows(int L);
+
+/* The KV pyramid (the _forward wrapper's pad_to_multiple + pooling x3, :1239-1270, :1311-1320):
+ * k/v [B,H,L,D] with strides k_stride/v_stride (elements; batch, head, row), rows gathered through
+ * `rows` (reordered row g = caller row rows[g]; NULL = g) -> kpyr/vpyr [B,H,R,D] contiguous:
+ *   rows [0, Lpad)              level 1: the reordered rows, rows >= L ZERO (the kernel's masked
+ *                               loads of the tail block, :111, :126)
+ *   [Lpad, 3Lpad/2)             level 2: mean of reordered row pairs, rows >= L replicate row L-1
+ *   [3Lpad/2, 7Lpad/4)          level 4: mean of level-2 pairs, rounded per level like torch.mean
+ *   [7Lpad/4, 15Lpad/8)         level 8
+ * One pass reads every row once. */
+int vb_kv_pyramid(const void* k, const void* v, const int64_t* k_stride, const int64_t* v_stride,
+                  const int32_t* rows, int B, int H, int L, int D, int dtype, void* kpyr, void* vpyr,
+                  void* stream);
+
+/* transfer_attn_to_mask (Triton/cogvideo_newattn.py:154-207): po [B,H,nr,nc] contiguous storage
+ * dtype -> mask [B,H,nr,nc] uint8. Per row, the entry ranked r in descending order (ties: lower
+ * column first; the reference's torch.sort is unstable) gets band_value[b] of the LAST band b with
+ * floor(nc*band_start[b]) <= r < floor(nc*band_end[b]) (bounds computed in double, as Python does),
+ * else 0; then the last two columns and the last two rows are set to 1. n_bands <= 8, values in
+ * {0,1,2,4,8}; band arrays are HOST memory. nc <= 4096. */
+int vb_level_mask(const void* po, int B, int H, int nr, int nc, int n_bands, const int32_t* band_value,
+                  const double* band_start, const double* band_end, int dtype, uint8_t* mask,
+                  void* stream);
+
+/* Multi-level attention forward (_fwd_kernel, :338-692): queries q [B,H,L,D] (rows through q_rows as
+ * in vb_attn_fwd), keys/values the pyramids of vb_kv_pyramid, level_mask [B,H,nb,nb] (nb =
+ * ceil(L/128); entries other than 1,2,4,8 skip). out [B,H,L,D] written at q_rows[g]; lse (nullable,
+ * fp32 [B,H,L] in REORDERED row order) = m + ln(l) of the reference's (l, m) pair.
+ * ref_tail = 1 reproduces the reference on L % 128 != 0: a level-1 tail block's keys >= L are
+ * zero vectors that still take part (logit 0, value 0); ref_tail = 0 masks them. */
+typedef struct vb_ml_attn_args {
+  const void* q; int64_t q_stride[3];
+  const int32_t* q_rows;       /* [L] or NULL */
+  const void* kpyr; const void* vpyr;   /* [B,H,vb_kv_pyramid_rows(L),D] contiguous */
+  const uint8_t* level_mask; int64_t mask_stride[3];
+  void* out; int64_t out_stride[3];
+  float* lse;
+  int B, H, L, D;
+  float scale;                 /* <= 0 -> D^-1/2 */
+  int ref_tail;
+  int dtype;
+  int heavy_rows;              /* last q-block rows known to be dense (the forced rows): dispatched first */
+} vb_ml_attn_args;
+int vb_ml_attn_fwd(const vb_ml_attn_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

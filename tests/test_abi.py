@@ -43,9 +43,9 @@ def test_abi_version(lib):
 
 def test_struct_layouts_match_header():
     """sizeof/offsetof of vb_attn_args and vb_predict_args from gcc == the ctypes mirrors."""
-    from vblade._lib import AttnArgs, BwdArgs, PredictArgs
+    from vblade._lib import AttnArgs, BwdArgs, MlAttnArgs, PredictArgs
     structs = (("vb_attn_args", AttnArgs), ("vb_predict_args", PredictArgs),
-               ("vb_attn_bwd_args", BwdArgs))
+               ("vb_attn_bwd_args", BwdArgs), ("vb_ml_attn_args", MlAttnArgs))
     fields = {st: [f[0] for f in cls._fields_] for st, cls in structs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for st, fl in fields.items():
@@ -107,6 +107,22 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     rc = lib.vb_block_sparse_attn_bwd(*([None] * 11), 1, 1, 64, 128, 128, 0.1, 0.0, 0, 0, 1, 0,
                                       None, None, None, None, 0, None)
     assert rc == _lib.VB_ERR_UNSUPPORTED and b"dropout" in lib.vb_last_error()
+    # multi-level entry points
+    assert lib.vb_kv_pyramid_rows(17776) == 15 * 17792 // 8
+    assert lib.vb_kv_pyramid_rows(128) == 240
+    m = _lib.MlAttnArgs()
+    assert lib.vb_ml_attn_fwd(ctypes.byref(m), None) == _lib.VB_ERR_INVALID
+    m.B = m.H = 1
+    m.L = 300
+    m.D = 80
+    m.q = m.kpyr = m.vpyr = m.level_mask = m.out = 16
+    assert lib.vb_ml_attn_fwd(ctypes.byref(m), None) == _lib.VB_ERR_UNSUPPORTED
+    assert lib.vb_kv_pyramid(None, None, None, None, None, 1, 1, 1, 64, 0, None, None, None) == _lib.VB_ERR_INVALID
+    vals = np.array([3], dtype=np.int32)
+    se = np.array([0.0, 1.0], dtype=np.float64)
+    rc = lib.vb_level_mask(16, 1, 1, 4, 4, 1, vals.ctypes.data, se[:1].ctypes.data, se[1:].ctypes.data,
+                           0, 16, None)
+    assert rc == _lib.VB_ERR_INVALID and b"band values" in lib.vb_last_error()
 
 
 def test_ops_refuse_cpu_tensors():

@@ -43,7 +43,7 @@ __device__ __forceinline__ unsigned long long vb_stamp() {
 #define VB_ACC(i, d)
 #endif
 
-template <int D, class T, bool kPool, bool kKvRows>
+template <int D, class T, bool kPool, bool kKvRows, bool kML = false>
 __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) attn_fwd_kernel(const FwdParams p) {
   constexpr int KS = D / 16;                   // k-steps of the QK^T product
   constexpr int DT = D / 32;                   // 32-wide d tiles of the output
@@ -56,6 +56,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   constexpr int kInstPerMat = kMatBytes / 1024;
   constexpr int kInstPerWave = 2 * kInstPerMat / 4;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kBufs * kBufBytes + kMaxBlocks * 2 + 16];
+  static_assert(!(kML && (kPool || kKvRows)), "multi-level mode reads the KV pyramids only");
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
   int* list_n = reinterpret_cast<int*>(smem + kBufs * kBufBytes + kMaxBlocks * 2);
 
@@ -110,7 +111,33 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       mrow = mh + (int64_t)qblk * p.ms[2];
     }
   }
-  if (threadIdx.x < 64) {
+  if (kML) {
+    // multi-level: per-level lists of key blocks (levels 1, 2, 4, 8, in that order), built in two
+    // passes over the mask row (counts, then positions) so they share the one kMaxBlocks array
+    if (threadIdx.x < 64) {
+      int cnt[4] = {0, 0, 0, 0};
+      for (int j0 = 0; j0 < nbk; j0 += 64) {
+        const int j = j0 + lane;
+        const int lv = j < nbk ? mrow[j] : 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cnt[e] += __popcll(__ballot(lv == (1 << e)));
+      }
+      int pos[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+      for (int j0 = 0; j0 < nbk; j0 += 64) {
+        const int j = j0 + lane;
+        const int lv = j < nbk ? mrow[j] : 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned long long bal = __ballot(lv == (1 << e));
+          if (lv == (1 << e))
+            list[pos[e] + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] = (uint16_t)j;
+          pos[e] += __popcll(bal);
+        }
+      }
+      if (lane < 4) list_n[lane] = cnt[0] * (lane == 0) + cnt[1] * (lane == 1) + cnt[2] * (lane == 2) + cnt[3] * (lane == 3);
+    }
+  } else if (threadIdx.x < 64) {
     int n = 0;
     if (p.use_main) {
       for (int j0 = 0; j0 < nbk; j0 += 64) {
@@ -149,9 +176,19 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
   // main tiles: two 64-key halves per kept block, minus an empty second half of the last block
   int ntm = 2 * nkept;
-  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kQBlk + kKT >= Lk) ntm -= 1;
+  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kQBlk + kKT >= Lk && !(kML && p.ref_tail)) ntm -= 1;
   const int ntp = kPool ? (p.Lkp + kKT - 1) / kKT : 0;
-  const int ntiles = ntm + ntp;
+  // multi-level tiles (64 pyramid rows, one level each): level 1 as above, one tile per level-2
+  // block, two level-4 blocks and four level-8 blocks per tile (a short last tile is masked)
+  int n2 = 0, n4 = 0, n8 = 0, T12 = 0, T124 = 0;
+  if (kML) {
+    n2 = __builtin_amdgcn_readfirstlane(list_n[1]);
+    n4 = __builtin_amdgcn_readfirstlane(list_n[2]);
+    n8 = __builtin_amdgcn_readfirstlane(list_n[3]);
+    T12 = ntm + n2;
+    T124 = T12 + (n4 + 1) / 2;
+  }
+  const int ntiles = kML ? T124 + (n8 + 3) / 4 : ntm + ntp;
 
   const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + krow0 * p.ks[2]);
   const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + krow0 * p.vs[2]);
@@ -176,6 +213,53 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       s.klen = min(kKT, p.Lkp - s.kstart);
     }
     return s;
+  };
+
+  // multi-level: pyramid rows of tile t's two quarters for this wave's half (packed block ids `raw`
+  // from ml_list_at, read one tile ahead like list_at)
+  const int off4 = p.Lpad + p.Lpad / 2, off8 = off4 + p.Lpad / 4;
+  const int my_half = (wave & 1) * 32;
+  auto ml_tile_src = [&](int t, int raw) __attribute__((always_inline)) -> MlTileSrc {
+    MlTileSrc s;
+    const int a = __builtin_amdgcn_readfirstlane(raw & 0xFFFF);
+    const int c = __builtin_amdgcn_readfirstlane(raw >> 16);
+    if (t < ntm) {
+      const int kstart = a * kQBlk + (t & 1) * kKT;
+      s.srcA = kstart + my_half;
+      s.klen = p.ref_tail ? kKT : min(kKT, Lk - kstart);
+      s.lvl = 0;
+    } else if (t < T12) {
+      s.srcA = p.Lpad + a * 64 + my_half;
+      s.klen = kKT;
+      s.lvl = 1;
+    } else if (t < T124) {
+      s.srcA = off4 + a * 32;
+      s.klen = min(kKT, (n4 - 2 * (t - T12)) * 32);
+      s.lvl = 2;
+    } else {
+      s.srcA = off8 + a * 16;
+      s.klen = min(kKT, (n8 - 4 * (t - T124)) * 16);
+      s.lvl = 3;
+    }
+    s.srcB = (t >= T124) ? off8 + c * 16 : s.srcA + 16;
+    return s;
+  };
+  auto ml_list_at = [&](int t) __attribute__((always_inline)) -> int {
+    int e0, e1;
+    if (t < ntm) {
+      e0 = e1 = t >> 1;
+    } else if (t < T12) {
+      e0 = e1 = nkept + (t - ntm);
+    } else if (t < T124) {
+      e0 = e1 = nkept + n2 + min(2 * (t - T12) + (wave & 1), n4 - 1);
+    } else {
+      const int e = 4 * (t - T124) + 2 * (wave & 1);
+      e0 = nkept + n2 + n4 + min(e, n8 - 1);
+      e1 = nkept + n2 + n4 + min(e + 1, n8 - 1);
+    }
+    e0 = min(max(e0, 0), kMaxBlocks - 1);
+    e1 = min(max(e1, 0), kMaxBlocks - 1);
+    return (int)list[e0] | ((int)list[e1] << 16);
   };
 
   // Tile t -> LDS ring slot t % kBufs by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
@@ -211,14 +295,24 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   // The host guarantees every slice spans < 2^31 bytes.
   const int my_rowb = (int)my_stride;
   const int my_prowb = (int)my_pstride;
-  const srd_t my_rsrc = make_srd(my_base, p.use_main ? (int)((int64_t)(Lk - 1) * my_stride + kRowB) : 0);
+  const int src_rows = kML ? 15 * (p.Lpad / 8) : Lk;   // pyramid rows in multi-level mode
+  const srd_t my_rsrc = make_srd(my_base, p.use_main ? (int)((int64_t)(src_rows - 1) * my_stride + kRowB) : 0);
   const srd_t my_prsrc = make_srd(kPool ? my_pbase : my_base, kPool ? (int)((int64_t)(p.Lkp - 1) * my_pstride + kRowB) : 0);
   int my_voff[kInstPerWave], my_pvoff[kInstPerWave];
 #pragma unroll
   for (int i = 0; i < kInstPerWave; ++i) {
-    my_voff[i] = my_row[i] * my_rowb + my_chunk[i] * 16;
+    // multi-level: rows relative to the instruction's 16-row quarter (its start is the soffset)
+    my_voff[i] = (kML ? (my_row[i] & 15) : my_row[i]) * my_rowb + my_chunk[i] * 16;
     my_pvoff[i] = my_row[i] * my_prowb + my_chunk[i] * 16;
   }
+  auto ml_issue = [&](const MlTileSrc src, int slot) __attribute__((always_inline)) {
+    uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
+    const int soffA = __builtin_amdgcn_readfirstlane(src.srcA * my_rowb);
+    const int soffB = __builtin_amdgcn_readfirstlane(src.srcB * my_rowb);
+#pragma unroll
+    for (int i = 0; i < kInstPerWave; ++i)
+      dma16(my_rsrc, dst + i * 1024, my_voff[i], (i * kRowsPerInst >= 16) ? soffB : soffA);
+  };
   auto issue = [&](const TileSrc src, int slot) __attribute__((always_inline)) {
     uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
     const bool pooled = kPool && src.pooled;
@@ -413,14 +507,27 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   auto list_at = [&](int t) __attribute__((always_inline)) -> int {
     return t < ntm ? (int)list[min(t >> 1, kMaxBlocks - 1)] : 0;
   };
-  TileSrc slot_src[kBufs];
-  slot_src[0] = tile_src(0, list_at(0));
-  if (ntiles > 0) issue(slot_src[0], 0);
+  using Src = std::conditional_t<kML, MlTileSrc, TileSrc>;
+  auto any_list_at = [&](int t) __attribute__((always_inline)) -> int {
+    if constexpr (kML) return ml_list_at(t);
+    else return list_at(t);
+  };
+  auto any_tile_src = [&](int t, int raw) __attribute__((always_inline)) -> Src {
+    if constexpr (kML) return ml_tile_src(t, raw);
+    else return tile_src(t, raw);
+  };
+  auto any_issue = [&](const Src src, int slot) __attribute__((always_inline)) {
+    if constexpr (kML) ml_issue(src, slot);
+    else issue(src, slot);
+  };
+  Src slot_src[kBufs];
+  slot_src[0] = any_tile_src(0, any_list_at(0));
+  if (ntiles > 0) any_issue(slot_src[0], 0);
   if constexpr (kBufs > 2) {
-    slot_src[1] = tile_src(1, list_at(1));
-    if (ntiles > 1) issue(slot_src[1], 1);
+    slot_src[1] = any_tile_src(1, any_list_at(1));
+    if (ntiles > 1) any_issue(slot_src[1], 1);
   }
-  int next_blk = list_at(kBufs - 1);
+  int next_blk = any_list_at(kBufs - 1);
   // The loop body is instantiated once per ring slot (compile-time U), so every LDS address is a
   // loop-invariant lane base + immediate offset: no address VALU inside the loop.
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
@@ -439,14 +546,16 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     VB_ACC(0, st1 - st0);
     const int ti = t + kBufs - 1;
     if (ti < ntiles) {
-      slot_src[un] = tile_src(ti, next_blk);
-      issue(slot_src[un], un);
-      next_blk = list_at(ti + 1);   // in flight during this tile's compute
+      slot_src[un] = any_tile_src(ti, next_blk);
+      any_issue(slot_src[un], un);
+      next_blk = any_list_at(ti + 1);   // in flight during this tile's compute
     }
     VB_STAMP(st2);
     VB_ACC(1, st2 - st1);
-    const TileSrc src = slot_src[u];
-    const float bias = (kPool && src.pooled) ? p.pool_bias_l2 : 0.f;
+    const Src src = slot_src[u];
+    float bias;
+    if constexpr (kML) bias = (float)src.lvl;   // + ln(p) in the exp2 domain: log2(p)
+    else bias = (kPool && src.pooled) ? p.pool_bias_l2 : 0.f;
     if (VB_DIAG && (p.dbg & 2)) return;   // diagnostic: stream tiles only
     tile_step(U, bias, src.klen);
     VB_STAMP(st3);
@@ -590,6 +699,60 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
   if (const char* d = getenv("VB_DEBUG_ATTN")) p.dbg = atoi(d);
 #endif
   return dispatch_fwd(p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int vb_kv_pyramid_rows(int L) {
+  const int lpad = (L + vb::kQBlk - 1) / vb::kQBlk * vb::kQBlk;
+  return 15 * (lpad / 8);
+}
+
+extern "C" int vb_ml_attn_fwd(const vb_ml_attn_args* a, void* stream) {
+  using namespace vb;
+  if (!a) return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: null args");
+  if (a->B <= 0 || a->H <= 0 || a->L <= 0) return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: B, H, L must be positive");
+  if (!a->q || !a->kpyr || !a->vpyr || !a->level_mask || !a->out)
+    return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: missing q/kpyr/vpyr/level_mask/out");
+  if (a->D != 64 && a->D != 128)
+    return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_fwd: head_dim must be 64 or 128, got " + std::to_string(a->D));
+  const int nb = (a->L + kQBlk - 1) / kQBlk;
+  if (nb > kMaxBlocks) return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_fwd: L too long");
+  for (int i = 0; i < 3; ++i)
+    if ((a->q_stride[i] | a->out_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: q/out strides must be multiples of 8 elements");
+  const int R = vb_kv_pyramid_rows(a->L);
+  if ((int64_t)R * 2 * a->D >= (int64_t(1) << 31)) return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_fwd: a pyramid (b,h) slice spans >= 2 GiB");
+  if (!aligned16(a->q) || !aligned16(a->out) || !aligned16(a->kpyr) || !aligned16(a->vpyr))
+    return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: tensors must be 16-byte aligned");
+  FwdParams p{};
+  p.q = a->q; p.k = a->kpyr; p.v = a->vpyr;
+  for (int i = 0; i < 3; ++i) {
+    p.qs[i] = a->q_stride[i]; p.os[i] = a->out_stride[i]; p.ms[i] = a->mask_stride[i];
+  }
+  p.ks[0] = p.vs[0] = (int64_t)a->H * R * a->D;
+  p.ks[1] = p.vs[1] = (int64_t)R * a->D;
+  p.ks[2] = p.vs[2] = a->D;
+  p.q_rows = a->q_rows;
+  p.use_main = 1;
+  p.mask = a->level_mask;
+  p.out = a->out; p.lse = a->lse;
+  p.lse_s[0] = (int64_t)a->H * a->L; p.lse_s[1] = a->L;
+  p.B = a->B; p.H = a->H; p.Lq = a->L; p.Lk = a->L; p.nbq = nb; p.nbk = nb;
+  p.Lpad = nb * kQBlk;
+  p.ref_tail = a->ref_tail ? 1 : 0;
+  const float scale = a->scale > 0.f ? a->scale : (float)(1.0 / sqrt((double)a->D));
+  p.c = scale * kLog2e;
+  p.heavy_rows = a->heavy_rows;
+  const dim3 grid(p.nbq * p.B * p.H);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a->dtype == VB_DTYPE_BF16) {
+    if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, BF16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, BF16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+  } else if (a->dtype == VB_DTYPE_F16) {
+    if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, F16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, F16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+  } else {
+    return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: unknown dtype");
+  }
+  return check_launch("attn_fwd_kernel (multi-level)");
 }
 
 extern "C" int vb_block_sparse_attn_fwd(const void* q_unpad, const void* k_unpad, const void* v_unpad,

@@ -19,6 +19,9 @@ struct FwdParams {
   int B, H, Lq, Lk, nbq, nbk;
   float c;                                    // softmax scale * log2(e)
   int heavy_rows;                             // last q-block rows known to be dense (scheduling hint)
+  // multi-level mode (vb_ml_attn_fwd): k/v are the KV pyramids [B,H,15*Lpad/8,D]
+  int Lpad;                                   // level-1 rows (ceil(L/128)*128)
+  int ref_tail;                               // 1: level-1 tail keys >= L take part (zero rows)
   int dbg;                                    // diagnostic builds only (VB_DEBUG_ATTN)
 };
 
@@ -68,6 +71,15 @@ struct TileSrc {
   int pooled;   // 0 = main (block-masked) keys, 1 = pooled keys
   int kstart;   // first key (reordered index for main, pooled index otherwise)
   int klen;     // valid keys in this tile (1..64)
+};
+
+// Multi-level tile: 64 pyramid rows of one level. The rows this wave's LDS-DMA fills (its half of
+// the tile, 32 rows) come as two 16-row quarters starting at pyramid rows srcA and srcB: a level-8
+// block is 16 rows, a level-4 block 32, levels 1/2 are contiguous.
+struct MlTileSrc {
+  int srcA, srcB;   // pyramid rows of this wave's first and second 16-row quarter
+  int klen;         // valid keys in this tile (1..64); the rest are masked
+  int lvl;          // log2 of the level: the logit bias in the exp2 domain
 };
 
 }  // namespace vb

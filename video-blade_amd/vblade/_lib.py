@@ -82,6 +82,23 @@ class BwdArgs(ctypes.Structure):
     ]
 
 
+class MlAttnArgs(ctypes.Structure):
+    """vb_ml_attn_args (include/vblade.h)."""
+    _fields_ = [
+        ("q", _vp), ("q_stride", _i64x3),
+        ("q_rows", _vp),
+        ("kpyr", _vp), ("vpyr", _vp),
+        ("level_mask", _vp), ("mask_stride", _i64x3),
+        ("out", _vp), ("out_stride", _i64x3),
+        ("lse", _vp),
+        ("B", ctypes.c_int), ("H", ctypes.c_int), ("L", ctypes.c_int), ("D", ctypes.c_int),
+        ("scale", ctypes.c_float),
+        ("ref_tail", ctypes.c_int),
+        ("dtype", ctypes.c_int),
+        ("heavy_rows", ctypes.c_int),
+    ]
+
+
 # name -> (restype, argtypes); must list every symbol include/vblade.h declares
 SIGNATURES = {
     "vb_last_error": (ctypes.c_char_p, []),
@@ -110,6 +127,14 @@ SIGNATURES = {
         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    "vb_kv_pyramid_rows": (ctypes.c_int, [ctypes.c_int]),
+    "vb_kv_pyramid": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        ctypes.c_int, _vp, _vp, _vp]),
+    "vb_level_mask": (ctypes.c_int, [
+        _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp,
+        ctypes.c_int, _vp, _vp]),
+    "vb_ml_attn_fwd": (ctypes.c_int, [ctypes.POINTER(MlAttnArgs), _vp]),
     "vb_lse_combine": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_float, ctypes.c_int, _vp, _vp, _vp]),

@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import AttnArgs, BwdArgs, PredictArgs, check
+from ._lib import AttnArgs, BwdArgs, MlAttnArgs, PredictArgs, check
 
 BLOCK = 128
 
@@ -374,6 +374,92 @@ def lse_combine(out1, lse1, out2, lse2, gap: float):
                                      out.data_ptr(), alpha.data_ptr(), _stream(dev)),
           "vb_lse_combine")
     return out, alpha
+
+
+# ----------------------------------------------------------------------------------------------
+# multi-level path (Triton/cogvideo_newattn.py + kernels/block_sparse_attn_kernel_with_backward_9_10.py)
+# ----------------------------------------------------------------------------------------------
+# Triton/cogvideo_newattn.py:12-18
+ML_MASK_RATIOS = {1: (0.0, 0.05), 2: (0.05, 0.15), 4: (0.15, 0.25), 8: (0.25, 0.5), 0: (0.5, 1.0)}
+
+
+def kv_pyramid_rows(L: int) -> int:
+    return int(_lib.load().vb_kv_pyramid_rows(int(L)))
+
+
+def kv_pyramid(k, v, rows=None):
+    """vb_kv_pyramid: K/V [B,H,L,D] (reordered through `rows`) -> pyramids [B,H,15*Lpad/8,D]:
+    level-1 rows (zero beyond L), then the 2x, 4x, 8x mean-pooled rows (replicate padding)."""
+    dev = _require_gpu(k, v, rows)
+    k, v = _aligned_bhld(k), _aligned_bhld(v)
+    B, H, L, D = k.shape
+    R = kv_pyramid_rows(L)
+    kpyr = torch.empty(B, H, R, D, device=dev, dtype=k.dtype)
+    vpyr = torch.empty(B, H, R, D, device=dev, dtype=v.dtype)
+    check(_lib.load().vb_kv_pyramid(k.data_ptr(), v.data_ptr(), ctypes.cast(_s3(k), ctypes.c_void_p),
+                                    ctypes.cast(_s3(v), ctypes.c_void_p), _ptr(rows), B, H, L, D,
+                                    _dtype_code(k), kpyr.data_ptr(), vpyr.data_ptr(), _stream(dev)),
+          "vb_kv_pyramid")
+    return kpyr, vpyr
+
+
+def pyramid_levels(pyr: torch.Tensor, L: int):
+    """Views [level1, level2, level4, level8] of a pyramid tensor (for tests and the backward)."""
+    Lpad = (L + BLOCK - 1) // BLOCK * BLOCK
+    offs = [0, Lpad, Lpad + Lpad // 2, Lpad + Lpad // 2 + Lpad // 4, 15 * Lpad // 8]
+    return [pyr[:, :, offs[i]:offs[i + 1]] for i in range(4)]
+
+
+def level_mask(po, ratios=None):
+    """vb_level_mask: transfer_attn_to_mask (Triton/cogvideo_newattn.py:154-207) on scores po
+    [B,H,nr,nc] -> uint8 levels (ties: lower column first)."""
+    dev = _require_gpu(po)
+    po = po.contiguous()
+    B, H, nr, nc = po.shape
+    ratios = ML_MASK_RATIOS if ratios is None else ratios
+    vals = np.array([int(v) for v in ratios], dtype=np.int32)
+    st = np.array([float(r[0]) for r in ratios.values()], dtype=np.float64)
+    en = np.array([float(r[1]) for r in ratios.values()], dtype=np.float64)
+    mask = torch.empty(B, H, nr, nc, device=dev, dtype=torch.uint8)
+    check(_lib.load().vb_level_mask(po.data_ptr(), B, H, nr, nc, len(vals), vals.ctypes.data,
+                                    st.ctypes.data, en.ctypes.data, _dtype_code(po), mask.data_ptr(),
+                                    _stream(dev)), "vb_level_mask")
+    return mask
+
+
+def ml_attention_fwd(q, kpyr, vpyr, level_mask_u8, *, q_rows=None, scale=None, ref_tail=True,
+                     want_lse=False, heavy_rows=2, out=None):
+    """vb_ml_attn_fwd: multi-level attention of q [B,H,L,D] over the KV pyramids. Returns out
+    (rows through q_rows) and, if want_lse, the fp32 natural-log LSE [B,H,L] (reordered rows)."""
+    dev = _require_gpu(q, kpyr, vpyr, level_mask_u8, q_rows)
+    q = _aligned_bhld(q)
+    B, H, L, D = q.shape
+    nb = (L + BLOCK - 1) // BLOCK
+    if tuple(level_mask_u8.shape) != (B, H, nb, nb) or level_mask_u8.dtype != torch.uint8:
+        raise ValueError(f"vblade: level mask must be uint8 [B,H,{nb},{nb}]")
+    R = kv_pyramid_rows(L)
+    for t in (kpyr, vpyr):
+        if tuple(t.shape) != (B, H, R, D) or not t.is_contiguous() or t.dtype != q.dtype:
+            raise ValueError(f"vblade: pyramids must be contiguous [B,H,{R},D] in q's dtype")
+    m = level_mask_u8
+    if m.stride(-1) != 1:
+        m = m.contiguous()
+    if out is None:
+        out = torch.empty_like(q) if q.is_contiguous() else torch.empty(B, H, L, D, device=dev, dtype=q.dtype)
+    lse = torch.empty(B, H, L, device=dev, dtype=torch.float32) if want_lse else None
+    a = MlAttnArgs()
+    a.q, a.q_stride, a.q_rows = q.data_ptr(), _s3(q), _ptr(q_rows)
+    a.kpyr, a.vpyr = kpyr.data_ptr(), vpyr.data_ptr()
+    a.level_mask = m.data_ptr()
+    a.mask_stride = (ctypes.c_int64 * 3)(m.stride(0), m.stride(1), m.stride(2))
+    a.out, a.out_stride, a.lse = out.data_ptr(), _s3(out), _ptr(lse)
+    a.B, a.H, a.L, a.D = B, H, L, D
+    a.scale = float(scale) if scale else 0.0
+    a.ref_tail = 1 if ref_tail else 0
+    a.dtype = _dtype_code(q)
+    a.heavy_rows = int(heavy_rows)
+    check(_lib.load().vb_ml_attn_fwd(ctypes.byref(a), _stream(dev)), "vb_ml_attn_fwd")
+    return (out, lse) if want_lse else out
 
 
 def default_scale(D: int) -> float:
