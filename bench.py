@@ -41,6 +41,10 @@ VARIANTS = {
                 video="13x30x45 latent tokens + 226 text"),
     "wan": dict(H=12, D=128, layers=30, frames=81, name="Wan2.1-1.3B 8-step 81x832x480 bf16",
                 video="21x30x52 latent tokens"),
+    # the VBench sampler's op (cogvideox/sample_evaluate/modify_cogvideo.py:9): multi-level mask
+    "cog-ml": dict(H=48, D=64, layers=42, frames=49,
+                   name="CogVideoX-5B 8-step 49x720x480 bf16, multi-level sampler path",
+                   video="13x30x45 latent tokens + 226 text"),
 }
 DENOISE_STEPS = 8
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
@@ -71,6 +75,20 @@ def realistic_qkv(H, L, D, seed, device):
     k = (torch.randn(1, H, L, D, generator=g, device=device) + 2 * cent).bfloat16()
     v = torch.randn(1, H, L, D, generator=g, device=device).bfloat16()
     return q, k, v
+
+
+def ml_attn_flops(mask: torch.Tensor, L: int, D: int) -> float:
+    """Algorithmic FLOPs of one multi-level launch: sum over (i,j) with level p in {1,2,4,8} of
+    4*m_i*(128/p)*D (m_i the true query-block size; key blocks are full pyramid blocks, as the
+    reference computes them)."""
+    nb = mask.shape[-1]
+    rows = torch.full((nb,), 128.0, device=mask.device)
+    rows[-1] = L - 128 * (nb - 1)
+    m = mask.to(torch.int32)
+    keys = torch.zeros_like(m, dtype=torch.float32)
+    for p in (1, 2, 4, 8):
+        keys += (m == p).float() * (128.0 / p)
+    return 4.0 * D * (rows[:, None] * keys).sum().item()
 
 
 def attn_flops(mask: torch.Tensor, L: int, D: int, Lkp: int) -> float:
@@ -122,7 +140,12 @@ def main():
     over = {}
     if args.density is not None:
         over = dict(min_retain_ratio=args.density, max_retain_ratio=args.density)
-    mod = vblade.AdaptiveBlockSparseAttn(args.variant, log_every=0, **over)
+    ml = args.variant == "cog-ml"
+    if ml:
+        from vblade import multilevel
+        mod = multilevel.AdaptiveBlockSparseAttnTrain(log_every=0)
+    else:
+        mod = vblade.AdaptiveBlockSparseAttn(args.variant, log_every=0, **over)
     L = mod.gilbert_rearranger.seq_len
     calls = DENOISE_STEPS * layers
     sets = [realistic_qkv(H, L, D, 1000 * rank + s, dev) for s in range(args.sets)]
@@ -158,7 +181,7 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     ms_per_call = ms_per_step / calls
     value = whole_job_frames_per_s(world, frames, args.steps, elapsed)
-    sparsity = mod.sparsity
+    sparsity = mod.sparsity_acc / mod.sparsity_counter if ml else mod.sparsity
 
     result = {
         "metric": "frames/sec/GPU, " + V["name"] + " (attention path); attn TFLOPS vs dense",
@@ -182,8 +205,9 @@ def main():
             "heads": H,
             "head_dim": D,
             "calls_per_step": calls,
-            "mask": "energy rule (reference defaults)" if args.density is None
-                    else f"fixed density {args.density}",
+            "mask": ("rank-band level mask, levels 1/2/4/8 (reference mask_ratios)" if ml
+                     else "energy rule (reference defaults)" if args.density is None
+                     else f"fixed density {args.density}"),
             "parallelism": f"replicas x{world} (prompt-batch DP, no collective)",
         },
         "ms_per_call": round(ms_per_call, 4),
@@ -207,7 +231,8 @@ def main():
                 result["roofline"]["traffic_detail"] = traffic
         result["roofline"]["algorithmic_bytes"] = extra["alg_bytes"]
         if not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(args.variant, calls, frames)
+            result["cpu_baseline"] = (cpu_baseline_ml(calls, frames) if ml
+                                      else cpu_baseline(args.variant, calls, frames))
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.barrier()
@@ -223,13 +248,20 @@ def measure_kernels(mod, sets, L, H, D, dev, args, events, rng_state, calls):
     ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
     torch.cuda.set_rng_state(rng_state, dev)
     flops = 0.0
-    Lkp = (L + mod.sample_gap - 1) // mod.sample_gap
+    ml = not hasattr(mod, "sample_gap")
+    Lkp = 0 if ml else (L + mod.sample_gap - 1) // mod.sample_gap
     n = 0
     for _ in range(args.steps):
         for c in range(calls):
             q, k, _ = sets[c % len(sets)]
-            _, mask = mod.predict_mask(q, k)
-            flops += attn_flops(mask, L, D, Lkp)
+            if ml:
+                from vblade import multilevel
+                _, mask = multilevel.predict_level_mask(q, k, rows=mod._rows(q.device),
+                                                        mask_ratios=mod.mask_ratios)
+                flops += ml_attn_flops(mask, L, D)
+            else:
+                _, mask = mod.predict_mask(q, k)
+                flops += attn_flops(mask, L, D, Lkp)
             n += 1
     assert n == len(events)
     flops /= n
@@ -251,6 +283,9 @@ def measure_kernels(mod, sets, L, H, D, dev, args, events, rng_state, calls):
     # compulsory bytes of one launch: Q read + O written once, every K/V row read at
     # least once (the kept blocks cover every key block), pooled K/V, the mask
     alg_bytes = H * (4 * L * D * 2) + H * 2 * Lkp * D * 2 + H * ((L + 127) // 128) ** 2
+    if ml:   # Q read + O written once, both KV pyramids (15/8 of the padded rows) read once, mask
+        R = 15 * ((L + 127) // 128 * 128) // 8
+        alg_bytes = H * (2 * L * D * 2) + H * 2 * R * D * 2 + H * ((L + 127) // 128) ** 2
     out = {"top": top, "alg_bytes": alg_bytes}
     if not args.no_dense:
         q, k, v = sets[0]
@@ -304,6 +339,37 @@ def pmc_traffic(variant, timeout=300):
             "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
             "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on tools/attn_only.py; "
                       "traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)"}
+
+
+def cpu_baseline_ml(calls, frames):
+    """The multi-level oracle (oracle/ml_oracle.py: sampler, pooled scores, level mask, pyramid,
+    multi-level softmax) timed on this host's cores: 2 heads of one call, scaled to a video."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bsa_oracle as O
+    import gilbert_oracle as G
+    import ml_oracle as ML
+    V = VARIANTS["cog-ml"]
+    heads = 2
+    rows = torch.from_numpy(G.full_sequence_perm(45, 30, 13, 226).astype("int64"))
+    L = rows.numel()
+    g = torch.Generator().manual_seed(0)
+    cent = torch.randn(1, heads, L // 128 + 1, V["D"], generator=g).repeat_interleave(128, 2)[:, :, :L]
+    q = (torch.randn(1, heads, L, V["D"], generator=g) + 2 * cent).bfloat16()
+    k = (torch.randn(1, heads, L, V["D"], generator=g) + 2 * cent).bfloat16()
+    v = torch.randn(1, heads, L, V["D"], generator=g).bfloat16()
+    qo = O.draw_sample_offsets(1, heads, generator=g)
+    ko = O.draw_sample_offsets(1, heads, generator=g)
+    t0 = time.perf_counter()
+    r = ML.adaptive_multilevel_attention(q[:, :, rows], k[:, :, rows], v[:, :, rows], qo, ko)
+    out = torch.empty_like(r["out"])
+    out[:, :, rows] = r["out"]
+    dt = time.perf_counter() - t0
+    t_call = dt * V["H"] / heads
+    return {"value": round(frames / (calls * t_call), 6), "unit": "frames/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"multi-level oracle (fp32 torch CPU), {heads} of {V['H']} heads of one "
+                      f"[1,{V['H']},{L},{V['D']}] call: {dt:.2f} s; scaled x{V['H'] // heads} heads "
+                      f"x {calls} calls per video"}
 
 
 def cpu_baseline(variant, calls, frames):

@@ -17,7 +17,22 @@ from bench import realistic_qkv  # noqa: E402
 variant = sys.argv[1] if len(sys.argv) > 1 else "cog"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 what = sys.argv[3] if len(sys.argv) > 3 else "attn"
-H, D = (48, 64) if variant == "cog" else (12, 128)
+H, D = (12, 128) if variant == "wan" else (48, 64)
+if variant == "cog-ml":   # the multi-level sampler path
+    from vblade import multilevel
+    m = multilevel.AdaptiveBlockSparseAttnTrain(log_every=0)
+    L = m.gilbert_rearranger.seq_len
+    dev = torch.device("cuda")
+    with torch.no_grad():
+        q, k, v = realistic_qkv(H, L, D, 0, dev)
+        rows = m._rows(dev)
+        _, mask = multilevel.predict_level_mask(q, k, rows=rows)
+        kp, vp = ops.kv_pyramid(k, v, rows)
+        for _ in range(n):
+            ops.ml_attention_fwd(q, kp, vp, mask, q_rows=rows, heavy_rows=2)
+        torch.cuda.synchronize()
+    print("done")
+    sys.exit(0)
 m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
 L = m.gilbert_rearranger.seq_len
 dev = torch.device("cuda")
