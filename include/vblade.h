@@ -257,7 +257,7 @@ int vb_level_mask(const void* po, int B, int H, int nr, int nc, int n_bands, con
 /* Multi-level attention forward (_fwd_kernel, :338-692): queries q [B,H,L,D] (rows through q_rows as
  * in vb_attn_fwd), keys/values the pyramids of vb_kv_pyramid, level_mask [B,H,nb,nb] (nb =
  * ceil(L/128); entries other than 1,2,4,8 skip). out [B,H,L,D] written at q_rows[g]; lse (nullable,
- * fp32 [B,H,L] in REORDERED row order) = m + ln(l) of the reference's (l, m) pair.
+ * fp32 [B,H,L] at the caller's row q_rows[g], as vb_attn_fwd) = m + ln(l) of the reference's (l, m).
  * ref_tail = 1 reproduces the reference on L % 128 != 0: a level-1 tail block's keys >= L are
  * zero vectors that still take part (logit 0, value 0); ref_tail = 0 masks them. */
 typedef struct vb_ml_attn_args {
@@ -274,6 +274,35 @@ typedef struct vb_ml_attn_args {
   int heavy_rows;              /* last q-block rows known to be dense (the forced rows): dispatched first */
 } vb_ml_attn_args;
 int vb_ml_attn_fwd(const vb_ml_attn_args* args, void* stream);
+
+/* Multi-level attention backward (_backward + the per-level kernels, :696-1237, :1375-1576),
+ * FlashAttention-2 semantics from the forward's out and lse, deterministic (no atomics):
+ *   dQ over every kept block's keys at its level (+ln p bias);
+ *   dK/dV of each pyramid row, the pooled levels' folded back through the means:
+ *   dk[r] = dK1[r] + dK2[r/2]/2 + dK4[r/4]/4 + dK8[r/8]/8 for r < L (gradient reaching the
+ *   replicate-padded rows is dropped, as the reference does).
+ * `rows` (nullable) is the reorder of the forward (pyramid rows and q_rows): q/out/dout/dq rows are
+ * addressed through it, and dk/dv of reordered key g are written at caller row rows[g].
+ * dq/dk/dv are fully overwritten. workspace >= vb_ml_attn_bwd_workspace_size(args) bytes. */
+typedef struct vb_ml_attn_bwd_args {
+  const void* q; int64_t q_stride[3];
+  const int32_t* rows;         /* [L] or NULL */
+  const void* kpyr; const void* vpyr;
+  const uint8_t* level_mask; int64_t mask_stride[3];
+  const void* out; int64_t out_stride[3];
+  const float* lse;            /* as vb_ml_attn_fwd wrote it */
+  const void* dout; int64_t dout_stride[3];
+  void* dq; int64_t dq_stride[3];
+  void* dk; void* dv; int64_t dk_stride[3]; int64_t dv_stride[3];
+  void* workspace; uint64_t workspace_bytes;
+  int B, H, L, D;
+  float scale;                 /* <= 0 -> D^-1/2 */
+  int ref_tail;
+  int dtype;
+  int heavy_rows;
+} vb_ml_attn_bwd_args;
+uint64_t vb_ml_attn_bwd_workspace_size(const vb_ml_attn_bwd_args* args);
+int vb_ml_attn_bwd(const vb_ml_attn_bwd_args* args, void* stream);
 
 #ifdef __cplusplus
 }

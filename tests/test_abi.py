@@ -43,9 +43,10 @@ def test_abi_version(lib):
 
 def test_struct_layouts_match_header():
     """sizeof/offsetof of vb_attn_args and vb_predict_args from gcc == the ctypes mirrors."""
-    from vblade._lib import AttnArgs, BwdArgs, MlAttnArgs, PredictArgs
+    from vblade._lib import AttnArgs, BwdArgs, MlAttnArgs, MlBwdArgs, PredictArgs
     structs = (("vb_attn_args", AttnArgs), ("vb_predict_args", PredictArgs),
-               ("vb_attn_bwd_args", BwdArgs), ("vb_ml_attn_args", MlAttnArgs))
+               ("vb_attn_bwd_args", BwdArgs), ("vb_ml_attn_args", MlAttnArgs),
+               ("vb_ml_attn_bwd_args", MlBwdArgs))
     fields = {st: [f[0] for f in cls._fields_] for st, cls in structs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for st, fl in fields.items():
@@ -117,6 +118,11 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     m.D = 80
     m.q = m.kpyr = m.vpyr = m.level_mask = m.out = 16
     assert lib.vb_ml_attn_fwd(ctypes.byref(m), None) == _lib.VB_ERR_UNSUPPORTED
+    mb = _lib.MlBwdArgs()
+    assert lib.vb_ml_attn_bwd(ctypes.byref(mb), None) == _lib.VB_ERR_INVALID
+    mb.B = mb.H = 1
+    mb.L, mb.D = 300, 64
+    assert lib.vb_ml_attn_bwd_workspace_size(ctypes.byref(mb)) > 7 * 384 // 8 * 64 * 4 * 2
     assert lib.vb_kv_pyramid(None, None, None, None, None, 1, 1, 1, 64, 0, None, None, None) == _lib.VB_ERR_INVALID
     vals = np.array([3], dtype=np.int32)
     se = np.array([0.0, 1.0], dtype=np.float64)

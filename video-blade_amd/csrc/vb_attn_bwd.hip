@@ -72,6 +72,26 @@ struct BwdParams {
   float c;      // scale * log2(e)
   float scale;
   int heavy_rows;
+  // multi-level mode (vb_ml_attn_bwd): k/v are the KV pyramids [B,H,15*Lpad/8,D] (contiguous),
+  // mask the level mask; the pooled levels' pyramid-row grads go to dkpyr/dvpyr fp32
+  // [B,H,7*Lpad/8,D] (level 2 rows, then level 4, then level 8)
+  int Lpad;
+  int ref_tail;
+  float* dkpyr; float* dvpyr;
+};
+
+// multi-level geometry shared by the backward kernels: pyramid level regions (rows) and the
+// pooled-level work items of the dK/dV pass (one 128-row pyramid block each)
+struct MlGeom {
+  int nb, Lpad, off[4];   // level-1/2/4/8 region starts in the pyramid
+  int nblk[4];            // 128-row pyramid blocks per level: ceil(nb / p)
+  __device__ __forceinline__ MlGeom(int Lpad_) {
+    Lpad = Lpad_;
+    nb = Lpad / 128;
+    off[0] = 0; off[1] = Lpad; off[2] = Lpad + Lpad / 2; off[3] = off[2] + Lpad / 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) nblk[e] = (nb + (1 << e) - 1) >> e;
+  }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -152,7 +172,7 @@ __global__ void __launch_bounds__(256) bwd_prep_kernel(const PrepParams p) {
 // ------------------------------------------------------------------------------------------------
 // dK / dV: one workgroup per (b, h, 128-key block)
 // ------------------------------------------------------------------------------------------------
-template <int D, class T, bool kPooled>
+template <int D, class T, bool kPooled, bool kML = false>
 __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kernel(const BwdParams p) {
   using namespace bwd;
   constexpr int KS = D / 16;
@@ -164,9 +184,10 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
   constexpr int kCh = RB / 16;
   constexpr int kInst = 2 * kInstTile + 1;  // Q, dO, stats (1 KiB)
   constexpr int kBufBytes = 2 * kTileBytes + 1024;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBufBytes + kMaxBlocks * 2 + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBufBytes + kMaxBlocks * 3 + 16];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + 2 * kBufBytes);
   int* list_n = reinterpret_cast<int*>(smem + 2 * kBufBytes + kMaxBlocks * 2);
+  uint8_t* list_bits = smem + 2 * kBufBytes + kMaxBlocks * 2 + 16;   // multi-level: active blocks
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -189,20 +210,55 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
     qrow0 = p.cu_q[b]; Lq = p.cu_q[b + 1] - p.cu_q[b];
     krow0 = p.cu_k[b]; Lk = p.cu_k[b + 1] - p.cu_k[b];
   }
-  const int Lkey = kPooled ? p.Lkp : Lk;
-  const int k0 = kblk * kBlk;
+  int Lkey = kPooled ? p.Lkp : Lk;
+  int k0 = kblk * kBlk;
+  // multi-level: level e (p = 2^e) of this work item, its pyramid region start and row count;
+  // pooled items number the level-2, then level-4, then level-8 pyramid blocks
+  int ml_e = 0, ml_m = kblk, ml_row0 = 0;
+  if (kML) {
+    const MlGeom gm(p.Lpad);
+    if (kPooled) {
+      ml_e = 1;
+      while (ml_e < 3 && ml_m >= gm.nblk[ml_e]) { ml_m -= gm.nblk[ml_e]; ++ml_e; }
+    }
+    ml_row0 = gm.off[ml_e];
+    Lkey = kPooled ? p.Lpad >> ml_e : Lk;
+    k0 = ml_m * kBlk;
+  }
   if (k0 >= Lkey || Lq <= 0) return;
   const int nbq = (Lq + kBlk - 1) / kBlk;
 
   bool nan_head = false;
   const uint8_t* mcol = nullptr;
-  if (!kPooled) {
+  if (!kPooled || kML) {
     const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
-    if (mh) mcol = mh + kblk;
+    if (mh) mcol = mh + (kML ? (ml_m << ml_e) : kblk);
   }
-  const int qlo = kPooled ? split * nbq / p.psplit : 0;
-  const int qhi = kPooled ? (split + 1) * nbq / p.psplit : nbq;
-  if (threadIdx.x < 64) {
+  const int qlo = (kPooled && !kML) ? split * nbq / p.psplit : 0;
+  const int qhi = (kPooled && !kML) ? (split + 1) * nbq / p.psplit : nbq;
+  if (kML) {
+    // q-blocks where any of this item's 2^e key blocks has level 2^e; bit e' = block ml_m*2^e + e'
+    if (threadIdx.x < 64) {
+      const int pl = 1 << ml_e;
+      const int nblk_here = min(pl, p.nbk - (ml_m << ml_e));
+      int n = 0;
+      for (int i0 = 0; i0 < nbq; i0 += 64) {
+        const int i = i0 + lane;
+        int bits = 0;
+        if (i < nbq)
+          for (int e = 0; e < nblk_here; ++e) bits |= (mcol[(int64_t)i * p.ms[2] + e] == pl) << e;
+        const unsigned long long bal = __ballot(bits != 0);
+        if (bits) {
+          const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+          list[pos] = (uint16_t)i;
+          list_bits[pos] = (uint8_t)bits;
+        }
+        n += __popcll(bal);
+      }
+      if (lane == 0) *list_n = n;
+    }
+  } else if (threadIdx.x < 64) {
     int n = 0;
     for (int i0 = qlo; i0 < qhi; i0 += 64) {
       const int i = i0 + lane;
@@ -222,12 +278,15 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
   const int key = k0 + wave * 32 + l32;
   const bool kvalid = key < Lkey;
   const int keyc = kvalid ? key : Lkey - 1;
-  const uint8_t* kb = kPooled
+  const uint8_t* kb = (kPooled && !kML)
       ? reinterpret_cast<const uint8_t*>(p.kp) + 2 * (b * p.kps[0] + h * p.kps[1] + (int64_t)keyc * p.kps[2])
-      : reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + (krow0 + keyc) * p.ks[2]);
-  const uint8_t* vb_ = kPooled
+      : reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + (krow0 + ml_row0 + keyc) * p.ks[2]);
+  const uint8_t* vb_ = (kPooled && !kML)
       ? reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1] + (int64_t)keyc * p.vps[2])
-      : reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + (krow0 + keyc) * p.vs[2]);
+      : reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + (krow0 + ml_row0 + keyc) * p.vs[2]);
+  // multi-level: which of the item's key blocks this lane's key belongs to, and the logit bias
+  const int my_blk_bit = kML ? (wave * 32 + l32) / (kBlk >> ml_e) : 0;
+  const float lvl_bias = (float)ml_e;
   typename T::vec8 kf[KS], vf[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -279,7 +338,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
     for (int r = 0; r < 16; ++r) dk[i][r] = dv[i][r] = 0.f;
 
   const int trr = tr_row(lane), trc = tr_col(lane);
-  constexpr int fL = kPooled ? 2 : 0;  // stats fields of this branch
+  constexpr int fL = (kPooled && !kML) ? 2 : 0;  // stats fields of this branch
   constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
   const bool many = wave < (kInst & 3);
 
@@ -296,6 +355,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
     const uint8_t* qt = smem + (t & 1) * kBufBytes;
     const uint8_t* dot = qt + kTileBytes;
     const float* st = reinterpret_cast<const float*>(qt + 2 * kTileBytes);
+    // multi-level pooled items: keys of blocks without level 2^e for this q-block take no part
+    bool act = true;
+    if (kML && kPooled) act = (list_bits[t >> 1] >> my_blk_bit) & 1;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       f32x16 s, dp;
@@ -314,7 +376,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * j + e;
-          const float pr = exp2_fast(fmaf(s[r], p.c, -Lv[e]));
+          float pr;
+          if (kML) pr = act ? exp2_fast(fmaf(s[r], p.c, lvl_bias - Lv[e])) : 0.f;
+          else pr = exp2_fast(fmaf(s[r], p.c, -Lv[e]));
           s[r] = pr;
           dp[r] = pr * (dp[r] - Dv[e]);
         }
@@ -342,6 +406,69 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
   // ---- epilogue: lane = key, registers = d ---------------------------------------------------------
   if (!kvalid) return;
   const float nanf_ = __builtin_nanf("");
+  if (kML && kPooled) {   // pooled pyramid rows: fp32 grads, summed into dk/dv by the level-1 pass
+    const int64_t po = (int64_t)bh * (7 * (p.Lpad / 8)) + (ml_row0 - p.Lpad) + key;
+    float* dkr = p.dkpyr + po * D;
+    float* dvr = p.dvpyr + po * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * half;
+        f32x4 a, c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = dk[dt][4 * g4 + e] * p.scale;
+          c[e] = dv[dt][4 * g4 + e];
+        }
+        *reinterpret_cast<f32x4*>(dkr + d) = a;
+        *reinterpret_cast<f32x4*>(dvr + d) = c;
+      }
+    return;
+  }
+  if (kML) {   // level-1 key (< L): + the mean-pool adjoints of its level-2/4/8 rows (KML:1494-1563)
+    const int64_t rb = (int64_t)bh * (7 * (p.Lpad / 8));
+    const float* pk[3];
+    const float* pv[3];
+#pragma unroll
+    for (int e = 1; e < 4; ++e) {
+      const int64_t row = rb + (MlGeom(p.Lpad).off[e] - p.Lpad) + (key >> e);
+      pk[e - 1] = p.dkpyr + row * D;
+      pv[e - 1] = p.dvpyr + row * D;
+    }
+    const int64_t orow = p.kv_rows ? p.kv_rows[key] : krow0 + key;
+    uint8_t* dkr = reinterpret_cast<uint8_t*>(p.dk) + 2 * (b * p.dks[0] + h * p.dks[1] + orow * p.dks[2]);
+    uint8_t* dvr = reinterpret_cast<uint8_t*>(p.dv) + 2 * (b * p.dvs[0] + h * p.dvs[1] + orow * p.dvs[2]);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * half;
+        float a[4], c[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = dk[dt][4 * g4 + e] * p.scale;
+          c[e] = dv[dt][4 * g4 + e];
+        }
+#pragma unroll
+        for (int lv = 0; lv < 3; ++lv) {
+          const float w = 1.0f / (float)(2 << lv);
+          const f32x4 x = *reinterpret_cast<const f32x4*>(pk[lv] + d);
+          const f32x4 y = *reinterpret_cast<const f32x4*>(pv[lv] + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] = fmaf(x[e], w, a[e]);
+            c[e] = fmaf(y[e], w, c[e]);
+          }
+        }
+        u32x2 w2, z;
+        w2[0] = pack2<T>(a[0], a[1]); w2[1] = pack2<T>(a[2], a[3]);
+        z[0] = pack2<T>(c[0], c[1]); z[1] = pack2<T>(c[2], c[3]);
+        *reinterpret_cast<u32x2*>(dkr + d * 2) = w2;
+        *reinterpret_cast<u32x2*>(dvr + d * 2) = z;
+      }
+    return;
+  }
   if (kPooled) {
     const int64_t po = ((int64_t)split * BH + bh) * p.Lkp + key;
     float* dkr = p.dkp_part + po * D;
@@ -412,7 +539,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 // ------------------------------------------------------------------------------------------------
 // dQ: one workgroup per (b, h, 128-row q-block); kept full-resolution tiles then pooled tiles
 // ------------------------------------------------------------------------------------------------
-template <int D, class T, bool kPool>
+template <int D, class T, bool kPool, bool kML = false>
 __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel(const BwdParams p) {
   using namespace bwd;
   constexpr int KS = D / 16;
@@ -465,7 +592,32 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
     const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
     if (mh) mrow = mh + (int64_t)qblk * p.ms[2];
   }
-  if (threadIdx.x < 64) {
+  if (kML) {
+    // per-level key-block lists (levels 1, 2, 4, 8 in that order; as the forward)
+    if (threadIdx.x < 64) {
+      int cnt[4] = {0, 0, 0, 0};
+      for (int j0 = 0; j0 < nbk; j0 += 64) {
+        const int j = j0 + lane;
+        const int lv = j < nbk ? mrow[j] : 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cnt[e] += __popcll(__ballot(lv == (1 << e)));
+      }
+      int pos[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+      for (int j0 = 0; j0 < nbk; j0 += 64) {
+        const int j = j0 + lane;
+        const int lv = j < nbk ? mrow[j] : 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned long long bal = __ballot(lv == (1 << e));
+          if (lv == (1 << e))
+            list[pos[e] + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] = (uint16_t)j;
+          pos[e] += __popcll(bal);
+        }
+      }
+      if (lane < 4) list_n[lane] = lane == 0 ? cnt[0] : lane == 1 ? cnt[1] : lane == 2 ? cnt[2] : cnt[3];
+    }
+  } else if (threadIdx.x < 64) {
     int n = 0;
     if (use_main) {
       for (int j0 = 0; j0 < nbk; j0 += 64) {
@@ -510,9 +662,40 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
   __syncthreads();
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
   int ntm = 2 * nkept;
-  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kBlk + kT >= Lk) ntm -= 1;
+  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kBlk + kT >= Lk && !(kML && p.ref_tail)) ntm -= 1;
   const int ntp = kPool ? (p.Lkp + kT - 1) / kT : 0;
-  const int ntiles = ntm + ntp;
+  // multi-level tiles (as the forward): level 1 (2 per block), one per level-2 block, two level-4
+  // blocks and four level-8 blocks per tile
+  int n2 = 0, n4 = 0, n8 = 0, T12 = 0, T124 = 0;
+  if (kML) {
+    n2 = __builtin_amdgcn_readfirstlane(list_n[1]);
+    n4 = __builtin_amdgcn_readfirstlane(list_n[2]);
+    n8 = __builtin_amdgcn_readfirstlane(list_n[3]);
+    T12 = ntm + n2;
+    T124 = T12 + (n4 + 1) / 2;
+  }
+  const int ntiles = kML ? T124 + (n8 + 3) / 4 : ntm + ntp;
+  // multi-level tile t: pyramid row of 16-row quarter qd, valid keys, level exponent
+  const int off4 = p.Lpad + p.Lpad / 2, off8 = off4 + p.Lpad / 4;
+  auto ml_quarter = [&](int t, int qd) __attribute__((always_inline)) -> int {
+    if (t < ntm) return (int)list[t >> 1] * kBlk + (t & 1) * kT + 16 * qd;
+    if (t < T12) return p.Lpad + (int)list[nkept + t - ntm] * 64 + 16 * qd;
+    if (t < T124) {
+      const int e = min(2 * (t - T12) + (qd >> 1), n4 - 1);
+      return off4 + (int)list[nkept + n2 + e] * 32 + 16 * (qd & 1);
+    }
+    const int e = min(4 * (t - T124) + qd, n8 - 1);
+    return off8 + (int)list[nkept + n2 + n4 + e] * 16;
+  };
+  auto ml_klen = [&](int t) __attribute__((always_inline)) -> int {
+    if (t < ntm) return p.ref_tail ? kT : min(kT, Lk - ((int)list[t >> 1] * kBlk + (t & 1) * kT));
+    if (t < T12) return kT;
+    if (t < T124) return min(kT, (n4 - 2 * (t - T12)) * 32);
+    return min(kT, (n8 - 4 * (t - T124)) * 16);
+  };
+  auto ml_lvl = [&](int t) __attribute__((always_inline)) -> int {
+    return t < ntm ? 0 : t < T12 ? 1 : t < T124 ? 2 : 3;
+  };
 
   const uint8_t* kbase = use_main ? reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + krow0 * p.ks[2]) : nullptr;
   const uint8_t* vbase = use_main ? reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + krow0 * p.vs[2]) : nullptr;
@@ -530,8 +713,14 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
     }
   };
   auto issue = [&](int t) __attribute__((always_inline)) {
-    int kstart, klen;
-    tile_keys(t, kstart, klen);
+    int kstart = 0, klen = kT;
+    int qsrc[4] = {0, 0, 0, 0};
+    if (kML) {
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) qsrc[qd] = __builtin_amdgcn_readfirstlane(ml_quarter(t, qd));
+    } else {
+      tile_keys(t, kstart, klen);
+    }
     const bool pooled = kPool && t >= ntm;
     uint8_t* buf = smem + (t & 1) * kBufBytes;
     for (int i = wave; i < kInst; i += 4) {
@@ -539,7 +728,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
       const int ii = isv ? i - kInstTile : i;
       const int r = ii * kRowsPerInst + lane / kCh;
       const int c = (lane % kCh) ^ dual_swz<D>(r);
-      const int64_t key = kstart + min(r, klen - 1);
+      const int64_t key = kML ? qsrc[r >> 4] + (r & 15) : kstart + min(r, klen - 1);
       const uint8_t* src;
       if (pooled) src = isv ? vpbase + key * 2 * p.vps[2] : kpbase + key * 2 * p.kps[2];
       else src = isv ? vbase + key * 2 * p.vs[2] : kbase + key * 2 * p.ks[2];
@@ -568,13 +757,20 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
     }
     __builtin_amdgcn_s_barrier();
     int kstart, klen;
-    tile_keys(t, kstart, klen);
-    const bool pooled = kPool && t >= ntm;
-    const float Lr = pooled ? L2 : L1;
+    float nL;
+    bool pooled;
+    if (kML) {
+      klen = ml_klen(t);
+      pooled = false;
+      nL = (float)ml_lvl(t) - L1;   // + log2(level): the +ln p logit bias in the exp2 domain
+    } else {
+      tile_keys(t, kstart, klen);
+      pooled = kPool && t >= ntm;
+      nL = -(pooled ? L2 : L1);
+    }
     const float Dr = pooled ? D2 : D1;
     const uint8_t* kt_ = smem + (t & 1) * kBufBytes;
     const uint8_t* vt_ = kt_ + kTileBytes;
-    const float nL = -Lr;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {   // 32-key halves: S^T, dP^T -> dS^T -> dQ^T
       f32x16 s, dp;
@@ -887,4 +1083,118 @@ extern "C" int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, c
   p.scale = softmax_scale > 0.f ? softmax_scale : (float)(1.0 / sqrt((double)head_dim));
   p.c = p.scale * kLog2e;
   return dispatch_bwd(pp, p, head_dim, dtype, false, reinterpret_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------------------------------------------------
+// multi-level backward (kernels/block_sparse_attn_kernel_with_backward_9_10.py _backward :1375-1576)
+// ------------------------------------------------------------------------------------------------
+namespace vb {
+struct MlWs {
+  uint64_t stats, q_r, do_r, dkpyr, dvpyr, total;
+};
+static MlWs ml_ws_layout(int B, int H, int L, int D, bool copies) {
+  auto up = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  MlWs w{};
+  const uint64_t ntile = (uint64_t)((L + 63) / 64);
+  const uint64_t lpad = (uint64_t)(L + 127) / 128 * 128;
+  uint64_t off = 0;
+  w.stats = off; off = up(off + (uint64_t)B * H * ntile * 256 * 4);
+  if (copies) {
+    w.q_r = off; off = up(off + (uint64_t)B * H * L * D * 2);
+    w.do_r = off; off = up(off + (uint64_t)B * H * L * D * 2);
+  }
+  w.dkpyr = off; off = up(off + (uint64_t)B * H * (7 * lpad / 8) * D * 4);
+  w.dvpyr = off; off = up(off + (uint64_t)B * H * (7 * lpad / 8) * D * 4);
+  w.total = off;
+  return w;
+}
+
+template <int D, class T>
+static int launch_ml_grads(const PrepParams& pp, const BwdParams& p, hipStream_t s) {
+  if (int rc = launch_prep<T>(pp, s)) return rc;
+  const int BH = p.B * p.H;
+  hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true, true>), dim3(p.nbkp * BH), dim3(bwd::kThreads), 0, s, p);
+  if (int rc = check_launch("bwd_dkdv_kernel<multi-level pooled>")) return rc;
+  hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, false, true>), dim3(p.nbk * BH), dim3(bwd::kThreads), 0, s, p);
+  if (int rc = check_launch("bwd_dkdv_kernel<multi-level>")) return rc;
+  hipLaunchKernelGGL((bwd_dq_kernel<D, T, false, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
+  return check_launch("bwd_dq_kernel<multi-level>");
+}
+}  // namespace vb
+
+extern "C" uint64_t vb_ml_attn_bwd_workspace_size(const vb_ml_attn_bwd_args* a) {
+  if (!a || a->B <= 0 || a->H <= 0 || a->L <= 0 || a->D <= 0) return 0;
+  return vb::ml_ws_layout(a->B, a->H, a->L, a->D, a->rows != nullptr).total;
+}
+
+extern "C" int vb_ml_attn_bwd(const vb_ml_attn_bwd_args* a, void* stream) {
+  using namespace vb;
+  if (!a) return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: null args");
+  if (a->B <= 0 || a->H <= 0 || a->L <= 0) return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: B, H, L must be positive");
+  if (a->D != 64 && a->D != 128)
+    return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_bwd: head_dim must be 64 or 128, got " + std::to_string(a->D));
+  if (a->dtype != VB_DTYPE_BF16 && a->dtype != VB_DTYPE_F16) return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: unknown dtype");
+  if (!a->q || !a->kpyr || !a->vpyr || !a->level_mask || !a->out || !a->lse || !a->dout || !a->dq || !a->dk || !a->dv)
+    return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: missing tensor");
+  const int nb = (a->L + 127) / 128;
+  if (nb > bwd::kMaxBlocks) return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_bwd: sequence too long");
+  const int64_t* strides[] = {a->q_stride, a->out_stride, a->dout_stride, a->dq_stride, a->dk_stride, a->dv_stride};
+  for (const int64_t* st : strides)
+    if (!mul8(st)) return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: strides must be multiples of 8 elements");
+  const void* ptrs[] = {a->q, a->kpyr, a->vpyr, a->out, a->dout, a->dq, a->dk, a->dv};
+  for (const void* q : ptrs)
+    if (!al16(q)) return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: tensors must be 16-byte aligned");
+  const MlWs w = ml_ws_layout(a->B, a->H, a->L, a->D, a->rows != nullptr);
+  if (!a->workspace || a->workspace_bytes < w.total || !al16(a->workspace))
+    return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: workspace missing or smaller than vb_ml_attn_bwd_workspace_size()");
+  uint8_t* ws = reinterpret_cast<uint8_t*>(a->workspace);
+  const int Lpad = nb * 128;
+  const int R = 15 * (Lpad / 8);
+
+  PrepParams pp{};
+  pp.q = a->q; pp.dout = a->dout; pp.out = a->out;
+  for (int i = 0; i < 3; ++i) { pp.qs[i] = a->q_stride[i]; pp.dos[i] = a->dout_stride[i]; pp.os[i] = a->out_stride[i]; }
+  pp.lse = a->lse;
+  pp.q_rows = a->rows;
+  pp.stats = reinterpret_cast<float*>(ws + w.stats);
+  if (a->rows) { pp.q_r = ws + w.q_r; pp.do_r = ws + w.do_r; }
+  pp.B = a->B; pp.H = a->H; pp.Lq = a->L; pp.D = a->D; pp.ntile = (a->L + 63) / 64;
+
+  BwdParams p{};
+  if (a->rows) {
+    p.q = ws + w.q_r; p.dout = ws + w.do_r;
+    p.qs[0] = p.dos[0] = (int64_t)a->H * a->L * a->D;
+    p.qs[1] = p.dos[1] = (int64_t)a->L * a->D;
+    p.qs[2] = p.dos[2] = a->D;
+  } else {
+    p.q = a->q; p.dout = a->dout;
+    for (int i = 0; i < 3; ++i) { p.qs[i] = a->q_stride[i]; p.dos[i] = a->dout_stride[i]; }
+  }
+  p.k = a->kpyr; p.v = a->vpyr;
+  p.ks[0] = p.vs[0] = (int64_t)a->H * R * a->D;
+  p.ks[1] = p.vs[1] = (int64_t)R * a->D;
+  p.ks[2] = p.vs[2] = a->D;
+  for (int i = 0; i < 3; ++i) {
+    p.ms[i] = a->mask_stride[i];
+    p.dqs[i] = a->dq_stride[i]; p.dks[i] = a->dk_stride[i]; p.dvs[i] = a->dv_stride[i];
+  }
+  p.mask = a->level_mask;
+  p.stats = pp.stats; p.ntile = pp.ntile;
+  p.dq = a->dq; p.q_rows = a->rows;
+  p.dk = a->dk; p.dv = a->dv; p.kv_rows = a->rows;
+  p.psplit = 1;
+  p.gap = 1;
+  p.B = a->B; p.H = a->H; p.Lq = a->L; p.Lk = a->L; p.nbq = nb; p.nbk = nb;
+  p.nbkp = (nb + 1) / 2 + (nb + 3) / 4 + (nb + 7) / 8;
+  p.Lpad = Lpad;
+  p.ref_tail = a->ref_tail ? 1 : 0;
+  p.dkpyr = reinterpret_cast<float*>(ws + w.dkpyr);
+  p.dvpyr = reinterpret_cast<float*>(ws + w.dvpyr);
+  p.scale = a->scale > 0.f ? a->scale : (float)(1.0 / sqrt((double)a->D));
+  p.c = p.scale * kLog2e;
+  p.heavy_rows = a->heavy_rows;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a->dtype == VB_DTYPE_BF16)
+    return a->D == 64 ? launch_ml_grads<64, BF16>(pp, p, st) : launch_ml_grads<128, BF16>(pp, p, st);
+  return a->D == 64 ? launch_ml_grads<64, F16>(pp, p, st) : launch_ml_grads<128, F16>(pp, p, st);
 }

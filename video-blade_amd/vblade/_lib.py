@@ -99,6 +99,27 @@ class MlAttnArgs(ctypes.Structure):
     ]
 
 
+class MlBwdArgs(ctypes.Structure):
+    """vb_ml_attn_bwd_args (include/vblade.h)."""
+    _fields_ = [
+        ("q", _vp), ("q_stride", _i64x3),
+        ("rows", _vp),
+        ("kpyr", _vp), ("vpyr", _vp),
+        ("level_mask", _vp), ("mask_stride", _i64x3),
+        ("out", _vp), ("out_stride", _i64x3),
+        ("lse", _vp),
+        ("dout", _vp), ("dout_stride", _i64x3),
+        ("dq", _vp), ("dq_stride", _i64x3),
+        ("dk", _vp), ("dv", _vp), ("dk_stride", _i64x3), ("dv_stride", _i64x3),
+        ("workspace", _vp), ("workspace_bytes", ctypes.c_uint64),
+        ("B", ctypes.c_int), ("H", ctypes.c_int), ("L", ctypes.c_int), ("D", ctypes.c_int),
+        ("scale", ctypes.c_float),
+        ("ref_tail", ctypes.c_int),
+        ("dtype", ctypes.c_int),
+        ("heavy_rows", ctypes.c_int),
+    ]
+
+
 # name -> (restype, argtypes); must list every symbol include/vblade.h declares
 SIGNATURES = {
     "vb_last_error": (ctypes.c_char_p, []),
@@ -135,6 +156,8 @@ SIGNATURES = {
         _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp,
         ctypes.c_int, _vp, _vp]),
     "vb_ml_attn_fwd": (ctypes.c_int, [ctypes.POINTER(MlAttnArgs), _vp]),
+    "vb_ml_attn_bwd_workspace_size": (ctypes.c_uint64, [ctypes.POINTER(MlBwdArgs)]),
+    "vb_ml_attn_bwd": (ctypes.c_int, [ctypes.POINTER(MlBwdArgs), _vp]),
     "vb_lse_combine": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_float, ctypes.c_int, _vp, _vp, _vp]),

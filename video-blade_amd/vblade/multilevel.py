@@ -75,23 +75,22 @@ class _SparseAttention(torch.autograd.Function):
     """The multi-level op with the reference kernel's autograd contract (:1580-1588)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, level_mask, sm_scale, ref_tail):
+    def forward(ctx, q, k, v, level_mask, sm_scale, ref_tail, rows=None):
         mask_u8 = level_mask.to(torch.uint8).contiguous()
-        kpyr, vpyr = ops.kv_pyramid(k, v)
-        out, lse = ops.ml_attention_fwd(q, kpyr, vpyr, mask_u8, scale=sm_scale, ref_tail=ref_tail,
-                                        want_lse=True)
-        ctx.save_for_backward(q, k, v, kpyr, vpyr, mask_u8, out, lse)
+        kpyr, vpyr = ops.kv_pyramid(k, v, rows)
+        out, lse = ops.ml_attention_fwd(q, kpyr, vpyr, mask_u8, q_rows=rows, scale=sm_scale,
+                                        ref_tail=ref_tail, want_lse=True)
+        ctx.save_for_backward(q, kpyr, vpyr, mask_u8, out, lse, rows)
         ctx.sm_scale = sm_scale
         ctx.ref_tail = ref_tail
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        from .backward import multilevel_attn_bwd
-        q, k, v, kpyr, vpyr, mask_u8, out, lse = ctx.saved_tensors
-        dq, dk, dv = multilevel_attn_bwd(dout, q, k, v, kpyr, vpyr, mask_u8, out, lse,
-                                         scale=ctx.sm_scale)
-        return dq, dk, dv, None, None, None
+        q, kpyr, vpyr, mask_u8, out, lse, rows = ctx.saved_tensors
+        dq, dk, dv = ops.ml_attention_bwd(dout.contiguous(), q, kpyr, vpyr, mask_u8, out, lse,
+                                          rows=rows, scale=ctx.sm_scale, ref_tail=ctx.ref_tail)
+        return dq, dk, dv, None, None, None, None
 
 
 def sparse_attention_factory(BLOCK_M=128, BLOCK_N=128, POOLING_BLOCK_N=128, ref_tail=True, **kwargs):
@@ -149,6 +148,19 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
             raise ValueError(f"sequence length {L} != {self.gilbert_rearranger.seq_len} expected "
                              f"by the Gilbert grid (width/height/depth/text_length)")
         rows = self._rows(q.device)
+        grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)
+        if grad:   # training: the autograd op (deterministic HIP backward), reorder inside it
+            with torch.no_grad():
+                if level_mask is None:
+                    _, mask = predict_level_mask(q.detach(), k.detach(), rows=rows,
+                                                 mask_ratios=self.mask_ratios, q_off=q_off, k_off=k_off)
+                else:
+                    mask = level_mask.to(torch.uint8).contiguous()
+            out = _SparseAttention.apply(q, k, v, mask, q.shape[-1] ** -0.5, self.ref_tail, rows)
+            self.last_mask = mask
+            self.sparsity_acc += 1.0 - density(self.mask_ratios)
+            self.sparsity_counter += 1
+            return out
         with torch.no_grad():
             if level_mask is None:
                 _, mask = predict_level_mask(q, k, rows=rows, mask_ratios=self.mask_ratios,

@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import AttnArgs, BwdArgs, MlAttnArgs, PredictArgs, check
+from ._lib import AttnArgs, BwdArgs, MlAttnArgs, MlBwdArgs, PredictArgs, check
 
 BLOCK = 128
 
@@ -460,6 +460,41 @@ def ml_attention_fwd(q, kpyr, vpyr, level_mask_u8, *, q_rows=None, scale=None, r
     a.heavy_rows = int(heavy_rows)
     check(_lib.load().vb_ml_attn_fwd(ctypes.byref(a), _stream(dev)), "vb_ml_attn_fwd")
     return (out, lse) if want_lse else out
+
+
+def ml_attention_bwd(dout, q, kpyr, vpyr, level_mask_u8, out, lse, *, rows=None, scale=None,
+                     ref_tail=True, heavy_rows=2):
+    """vb_ml_attn_bwd: gradients of the multi-level attention. q/out/dout [B,H,L,D] (rows through
+    ``rows``), pyramids and mask as the forward; lse as ml_attention_fwd(want_lse=True) wrote it.
+    Returns (dq, dk, dv) [B,H,L,D] in q's dtype (dk/dv at the caller's rows)."""
+    dev = _require_gpu(dout, q, kpyr, vpyr, level_mask_u8, out, lse, rows)
+    q, out, dout = _aligned_bhld(q), _aligned_bhld(out), _aligned_bhld(dout)
+    B, H, L, D = q.shape
+    m = level_mask_u8 if level_mask_u8.stride(-1) == 1 else level_mask_u8.contiguous()
+    lse = lse.float().contiguous()
+    dq = torch.empty(B, H, L, D, device=dev, dtype=q.dtype)
+    dk = torch.empty(B, H, L, D, device=dev, dtype=q.dtype)
+    dv = torch.empty(B, H, L, D, device=dev, dtype=q.dtype)
+    a = MlBwdArgs()
+    a.q, a.q_stride, a.rows = q.data_ptr(), _s3(q), _ptr(rows)
+    a.kpyr, a.vpyr = kpyr.data_ptr(), vpyr.data_ptr()
+    a.level_mask = m.data_ptr()
+    a.mask_stride = (ctypes.c_int64 * 3)(m.stride(0), m.stride(1), m.stride(2))
+    a.out, a.out_stride, a.lse = out.data_ptr(), _s3(out), lse.data_ptr()
+    a.dout, a.dout_stride = dout.data_ptr(), _s3(dout)
+    a.dq, a.dq_stride = dq.data_ptr(), _s3(dq)
+    a.dk, a.dv, a.dk_stride, a.dv_stride = dk.data_ptr(), dv.data_ptr(), _s3(dk), _s3(dv)
+    a.B, a.H, a.L, a.D = B, H, L, D
+    a.scale = float(scale) if scale else 0.0
+    a.ref_tail = 1 if ref_tail else 0
+    a.dtype = _dtype_code(q)
+    a.heavy_rows = int(heavy_rows)
+    lib = _lib.load()
+    nbytes = int(lib.vb_ml_attn_bwd_workspace_size(ctypes.byref(a)))
+    ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
+    check(lib.vb_ml_attn_bwd(ctypes.byref(a), _stream(dev)), "vb_ml_attn_bwd")
+    return dq, dk, dv
 
 
 def default_scale(D: int) -> float:
