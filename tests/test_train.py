@@ -1,0 +1,137 @@
+"""CPU: the TDM training-step integration (vblade.train) — LoRA layers, gradient checkpointing,
+the bucketed data-parallel gradient all-reduce (gloo, world size 2) and the diffusers LoRA
+checkpoint format. The attention inside is a CPU stand-in here (plain softmax attention); the
+GPU test (test_gpu_module.py) runs the same step through the HIP sparse attention."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+from vblade import train as T
+
+
+class CpuAttention(nn.Module):
+    def forward(self, q, k, v):
+        return F.scaled_dot_product_attention(q.float(), k.float(), v.float()).to(q.dtype)
+
+
+def _model(layers=2, hidden=64, heads=4, rank=4, ckpt=True, seed=0):
+    return T.StandInTransformer(layers, hidden, heads, rank, float(rank), CpuAttention(),
+                                gradient_checkpointing=ckpt, dtype=torch.float32, seed=seed)
+
+
+def _batch(n, L=32, hidden=64, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, L, hidden, generator=g), torch.randn(n, L, hidden, generator=g)
+
+
+def _perturb_b(model, seed=3):
+    # LoRA B starts at zero (so A gets no gradient on the first step); give it values
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if n.endswith("lora_B"):
+                p.copy_(torch.randn(p.shape, generator=g) * 0.05)
+
+
+def test_lora_linear_starts_as_the_base_layer():
+    lin = T.LoRALinear(8, 6, 2, 2.0, dtype=torch.float32, generator=torch.Generator().manual_seed(0))
+    x = torch.randn(3, 8)
+    assert torch.equal(lin(x), F.linear(x, lin.weight, lin.bias))
+    assert [n for n, p in lin.named_parameters() if p.requires_grad] == ["lora_A", "lora_B"]
+
+
+def test_gradient_checkpointing_gives_identical_grads():
+    grads = []
+    for ckpt in (False, True):
+        m = _model(ckpt=ckpt)
+        _perturb_b(m)
+        x, y = _batch(2)
+        T.pseudo_huber(m(x), y, 1e-3).backward()
+        grads.append([p.grad.clone() for p in m.lora_parameters()])
+    for a, b in zip(*grads):
+        assert torch.allclose(a, b, atol=1e-7, rtol=1e-6)
+
+
+def test_train_step_accumulation_equals_full_batch():
+    m1, m2 = _model(), _model()
+    _perturb_b(m1)
+    _perturb_b(m2)
+    x, y = _batch(4)
+    s1 = T.TrainStep(m1, lr=1e-2, accum=1)
+    s2 = T.TrainStep(m2, lr=1e-2, accum=2)
+    s1([(x, y)])
+    s2([(x[:2], y[:2]), (x[2:], y[2:])])
+    for a, b in zip(m1.lora_parameters(), m2.lora_parameters()):
+        assert torch.allclose(a, b, atol=1e-6, rtol=1e-5)
+
+
+def test_lora_checkpoint_round_trip_and_key_format(tmp_path):
+    m = _model()
+    _perturb_b(m)
+    path = T.save_lora_weights(str(tmp_path), m)
+    assert os.path.basename(path) == "pytorch_lora_weights.safetensors"
+    keys = set(T.lora_state_dict(m))
+    assert "transformer.transformer_blocks.0.attn1.to_q.lora_A.weight" in keys
+    assert "transformer.transformer_blocks.1.attn1.to_out.0.lora_B.weight" in keys
+    assert len(keys) == 2 * 4 * 2
+    m2 = _model(seed=9)
+    T.load_lora_weights(m2, str(tmp_path))
+    for a, b in zip(m.lora_parameters(), m2.lora_parameters()):
+        assert torch.equal(a, b)
+    bad = T.StandInTransformer(3, 64, 4, 4, 4.0, CpuAttention(), dtype=torch.float32)
+    with pytest.raises(KeyError):
+        T.load_lora_weights(bad, path)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = _model()
+    _perturb_b(m)
+    red = T.BucketedGradReducer(m.lora_parameters(), bucket_bytes=4096)   # several buckets
+    step = T.TrainStep(m, lr=1e-2, accum=2, reducer=red)
+    x, y = _batch(8)
+    xs, ys = x[4 * rank:4 * rank + 4], y[4 * rank:4 * rank + 4]   # this rank's shard
+    step([(xs[:2], ys[:2]), (xs[2:], ys[2:])])
+    q.put((rank, [p.detach().numpy().copy() for p in m.lora_parameters()], len(red.buckets)))
+    red.close()
+    dist.destroy_process_group()
+
+
+def test_two_rank_bucketed_all_reduce_equals_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (ps, nb)) for r, ps, nb in (q.get(timeout=180) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] > 1
+    # single process, whole batch, accumulation 4 x 2 samples = the same global mean
+    m = _model()
+    _perturb_b(m)
+    step = T.TrainStep(m, lr=1e-2, accum=2)
+    x, y = _batch(8)
+    step([(x[:4], y[:4]), (x[4:], y[4:])])
+    for a, b, c in zip(res[0][0], res[1][0], m.lora_parameters()):
+        a, b = torch.from_numpy(a), torch.from_numpy(b)
+        assert torch.equal(a, b)                       # ranks agree exactly
+        assert torch.allclose(a, c.detach(), atol=2e-6, rtol=1e-5)

@@ -275,6 +275,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     k_lane[ks] = l32 * kRowB + 16 * ((2 * ks + half) ^ sw);
   }
   uint16_t* Rq = p.rbuf + ((int64_t)bh * nb + (wave_active ? qb : 0)) * nb * 32;   // this q-block
+  const srd_t rsrd = make_srd(Rq, nb * 64);
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
@@ -287,34 +288,51 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     __builtin_amdgcn_s_barrier();
     if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
     const uint8_t* kl = ktile + u * kTileBytes;
-    float mx[kKT];
+    // one accumulator per 32-key block: the MFMAs of block kt+1 do not wait for the row-max
+    // reads of block kt (a shared accumulator serialises MFMA -> s_nop -> VALU -> MFMA)
+    f32x16 sc[kKT];
 #pragma unroll
     for (int kt = 0; kt < kKT; ++kt) {
       typename T::vec8 kf[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         kf[ks] = *reinterpret_cast<const typename T::vec8*>(kl + kt * 32 * kRowB + k_lane[ks]);
-      f32x16 sc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+      for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) sc = T::mfma32(kf[ks], qf[ks], sc);
-      float x = fmaxf(fmaxf(sc[0], sc[1]), sc[2]);
-#pragma unroll
-      for (int r = 3; r < 15; r += 2) x = fmaxf(fmaxf(x, sc[r]), sc[r + 1]);
-      x = fmaxf(x, sc[15]);
-      mx[kt] = max_xor32(x) * p.c;                   // tl.max(qk, 1) * qk_scale
+      for (int ks = 0; ks < KS; ++ks) sc[kt] = T::mfma32(kf[ks], qf[ks], sc[kt]);
     }
-    // every lane holds all kKT row maxima of its row; each store instruction writes two columns
-    // (half 0 the even, half 1 the odd one) as 128 contiguous bytes
+    // row maxima, two 32-key blocks per v_permlane32_swap: after the swap lanes 0-31 hold block
+    // 2pr's full row max and lanes 32-63 block 2pr+1's (the halves of each block's C tile meet)
     const int j0 = kKT * t;
-#pragma unroll
-    for (int kt = 0; kt < kKT; ++kt)
-      if (j0 + kt < nb) m = fmaxf(m, mx[kt]);
+    float mxp[kKT / 2];
 #pragma unroll
     for (int pr = 0; pr < kKT / 2; ++pr) {
-      const int j = j0 + 2 * pr + half;
-      if (j < nb && wave_active) Rq[j * 32 + l32] = (uint16_t)storage_bits<T>(half ? mx[2 * pr + 1] : mx[2 * pr]);
+      float x[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x16& a = sc[2 * pr + e];
+        float y = fmaxf(fmaxf(a[0], a[1]), a[2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) y = fmaxf(fmaxf(y, a[r]), a[r + 1]);
+        x[e] = fmaxf(y, a[15]);
+      }
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]), __float_as_uint(x[1]), false, false);
+      mxp[pr] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * p.c;   // tl.max(qk, 1) * qk_scale
+    }
+    if (j0 + kKT > nb) {   // partial last tile: blocks past nb take no part (their rows are zeros)
+      asm volatile("");
+#pragma unroll
+      for (int pr = 0; pr < kKT / 2; ++pr)
+        if (j0 + 2 * pr + half >= nb) mxp[pr] = -INFINITY;
+    }
+#pragma unroll
+    for (int pr = 0; pr < kKT / 2; ++pr) m = fmaxf(m, mxp[pr]);   // this half's blocks; halves meet below
+    // R[j][row]: lane (half, row) stores block j0 + 2pr + half, so one store writes 128 contiguous bytes
+    if (wave_active) {
+#pragma unroll
+      for (int pr = 0; pr < kKT / 2; ++pr)
+        if (j0 + 2 * pr + half < nb) store16(rsrd, (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
     }
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
@@ -325,6 +343,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
       if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
   }
   static_assert(kBufs == 3 || kBufs == 4, "the loop body is instantiated once per ring slot");
+  m = max_xor32(m);   // the two halves saw alternate key blocks
   if (half == 0) mrow_s[wave * 32 + l32] = m;
   __syncthreads();
   if (!wave_active || (VB_DIAG && (p.dbg & 1))) return;
@@ -336,11 +355,28 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   const float* mw = mrow_s + wave * 32;
   // this wave's R columns were stored by its own lanes: wait for them and drop any stale L1 line
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  float mreg[32];
+#pragma unroll
+  for (int r = 0; r < 32; r += 4) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(mw + r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mreg[r + e] = x[e];
+  }
   float part = 0.f;
   for (int j = lane; j < nb; j += 64) {
+    // the block's 32 row maxima: 64 contiguous bytes, four 16-byte loads in flight at once
+    u32x4 w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = reinterpret_cast<const u32x4*>(Rq + j * 32)[c];
     float cm = -INFINITY;
-#pragma unroll 8
-    for (int r = 0; r < 32; ++r) cm = fmaxf(cm, T::bits_to_f32(Rq[j * 32 + r]) - mw[r]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 8 * c + 2 * e;
+        cm = max3f(cm, T::bits_to_f32((uint16_t)(w[c][e] & 0xFFFF)) - mreg[r],
+                   T::bits_to_f32((uint16_t)(w[c][e] >> 16)) - mreg[r + 1]);
+      }
     cm = round_to<T>(exp2_fast(cm));
     val[j] = cm;
     part += cm;

@@ -95,6 +95,14 @@ __device__ __forceinline__ void dma16(srd_t srd, uint8_t* lds, int voffset, int 
       (__attribute__((address_space(3))) void*)lds, 16, voffset, soffset, 0, 0);
 }
 
+// 16-bit store through a buffer descriptor: lane address = base + voffset + soffset (no 64-bit
+// per-lane address arithmetic on the VALU)
+__device__ __forceinline__ void store16(srd_t srd, uint16_t v, int voffset, int soffset) {
+  __builtin_amdgcn_raw_buffer_store_b16(
+      v, __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(srd.base), (short)0, srd.bytes, 0x00020000),
+      voffset, soffset, 0);
+}
+
 // ---- dual-use LDS image ---------------------------------------------------------------------------
 // A [rows][D] 16-bit tile read BOTH row-wise (ds_read_b128: 16 lanes = 16 consecutive rows, one
 // 16-byte chunk) and transposed (ds_read_b64_tr_b16: a half-wave = 4 consecutive rows x 64 bytes),

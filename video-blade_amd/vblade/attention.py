@@ -116,7 +116,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
         if variant not in VARIANT_DEFAULTS:
             raise ValueError(f"variant must be one of {list(VARIANT_DEFAULTS)}")
         cfg = dict(VARIANT_DEFAULTS[variant])
-        unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep"}
+        unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep", "overlap"}
         if unknown:
             raise TypeError(f"unknown options {sorted(unknown)}")
         cfg.update(overrides)
@@ -145,6 +145,9 @@ class AdaptiveBlockSparseAttn(nn.Module):
         # optional list: when set, every fused attention launch is bracketed by a pair of HIP
         # events on the launch stream (bench.py's live kernel timing); None = no events
         self.attn_events: Optional[list] = None
+        # overlap the pooled K/V pass with the predictor on a second stream (inference only)
+        self.overlap = bool(cfg.get("overlap", True))
+        self._side = ops.SideStream()
 
     # -------------------------------------------------------------------------------- helpers
     def _rows(self, device):
@@ -210,6 +213,16 @@ class AdaptiveBlockSparseAttn(nn.Module):
         rows = self._rows(q.device)
         nb = (L + self.block - 1) // self.block
         count = self._count_slot(q.device)
+        grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)
+        # inference: the pooled K/V pass (HBM-bound) runs on a side stream beside the mask
+        # predictor (MFMA-bound); they are independent within the call
+        fused = not grad and self.combine != "reference"
+        pooled = None
+        if fused:
+            # one pass over K/V: pooled K/V + Gilbert-ordered contiguous copies the attention
+            # kernel streams by LDS-DMA (launched first so it runs beside the predictor)
+            side = self._side.fork(q.device) if self.overlap else None
+            pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True, stream=side)
         if block_mask is None:
             with torch.no_grad():
                 _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count)
@@ -219,14 +232,14 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self._slot_totals.append(B * H * nb * nb)
         self.sparsity_counter += 1
         self.last_mask = mask
-        grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)
-        if grad or self.combine == "reference":
+        if not fused:
             from .autograd import adaptive_split_attention
             out = adaptive_split_attention(q, k, v, mask, rows, self.sample_gap)
         else:
-            # one pass over K/V: pooled K/V + Gilbert-ordered contiguous copies the attention
-            # kernel streams by LDS-DMA; q rows gathered and out rows scattered in the kernel
-            kp, vp, k_r, v_r = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True)
+            # q rows gathered and out rows scattered inside the attention kernel
+            kp, vp, k_r, v_r = pooled
+            if self.overlap:
+                self._side.join(q.device)
             ev = self.attn_events
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)

@@ -114,7 +114,8 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
     mask_ratios). ``ref_tail`` keeps the reference kernel's level-1 tail behaviour (see
     include/vblade.h, vb_ml_attn_fwd)."""
 
-    def __init__(self, *, mask_ratios=None, ref_tail: bool = True, log_every: int = 600, **overrides):
+    def __init__(self, *, mask_ratios=None, ref_tail: bool = True, log_every: int = 600,
+                 overlap: bool = True, **overrides):
         super().__init__()
         cfg = dict(DEFAULTS)
         unknown = set(overrides) - set(cfg)
@@ -132,6 +133,8 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
         self.sparsity_counter = 0
         self.last_mask: Optional[torch.Tensor] = None
         self.attn_events: Optional[list] = None   # bench.py's live kernel timing (see attention.py)
+        self.overlap = bool(overlap)
+        self._side = ops.SideStream()
 
     def _rows(self, device):
         if not self.use_rearrange:
@@ -162,12 +165,16 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
             self.sparsity_counter += 1
             return out
         with torch.no_grad():
+            # the pyramid pass (HBM-bound) on a side stream beside the predictor (MFMA-bound)
+            side = self._side.fork(q.device) if self.overlap else None
+            kpyr, vpyr = ops.kv_pyramid(k, v, rows, stream=side)
             if level_mask is None:
                 _, mask = predict_level_mask(q, k, rows=rows, mask_ratios=self.mask_ratios,
                                              q_off=q_off, k_off=k_off)
             else:
                 mask = level_mask.to(torch.uint8).contiguous()
-            kpyr, vpyr = ops.kv_pyramid(k, v, rows)
+            if side is not None:
+                self._side.join(q.device)
             ev = self.attn_events
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)

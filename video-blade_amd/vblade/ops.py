@@ -340,10 +340,12 @@ def energy_mask(po, *, energy_threshold=0.95, min_keep=1, max_keep=1, force_tail
     return mask
 
 
-def pool_kv(k, v, gap: int, rows=None, reordered: bool = False):
+def pool_kv(k, v, gap: int, rows=None, reordered: bool = False, stream=None):
     """vb_pool_kv: mean over `gap` consecutive reordered tokens (replicate pad) -> kp, vp; with
     reordered=True also returns the Gilbert-ordered contiguous copies (k_r, v_r) written in the
-    same pass."""
+    same pass. ``stream`` (a torch.cuda.Stream) launches there instead of the current stream; the
+    outputs are still allocated on the current stream, which must wait for ``stream`` before
+    using them."""
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
     B, H, L, D = k.shape
@@ -355,7 +357,8 @@ def pool_kv(k, v, gap: int, rows=None, reordered: bool = False):
     check(_lib.load().vb_pool_kv(k.data_ptr(), v.data_ptr(), ctypes.cast(_s3(k), ctypes.c_void_p),
                                  ctypes.cast(_s3(v), ctypes.c_void_p), _ptr(rows), B, H, L, D,
                                  int(gap), _dtype_code(k), kp.data_ptr(), vp.data_ptr(),
-                                 _ptr(k_r), _ptr(v_r), _stream(dev)), "vb_pool_kv")
+                                 _ptr(k_r), _ptr(v_r),
+                                 stream.cuda_stream if stream is not None else _stream(dev)), "vb_pool_kv")
     if reordered:
         return kp, vp, k_r, v_r
     return kp, vp
@@ -387,9 +390,10 @@ def kv_pyramid_rows(L: int) -> int:
     return int(_lib.load().vb_kv_pyramid_rows(int(L)))
 
 
-def kv_pyramid(k, v, rows=None):
+def kv_pyramid(k, v, rows=None, stream=None):
     """vb_kv_pyramid: K/V [B,H,L,D] (reordered through `rows`) -> pyramids [B,H,15*Lpad/8,D]:
-    level-1 rows (zero beyond L), then the 2x, 4x, 8x mean-pooled rows (replicate padding)."""
+    level-1 rows (zero beyond L), then the 2x, 4x, 8x mean-pooled rows (replicate padding).
+    ``stream``: as pool_kv."""
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
     B, H, L, D = k.shape
@@ -398,7 +402,8 @@ def kv_pyramid(k, v, rows=None):
     vpyr = torch.empty(B, H, R, D, device=dev, dtype=v.dtype)
     check(_lib.load().vb_kv_pyramid(k.data_ptr(), v.data_ptr(), ctypes.cast(_s3(k), ctypes.c_void_p),
                                     ctypes.cast(_s3(v), ctypes.c_void_p), _ptr(rows), B, H, L, D,
-                                    _dtype_code(k), kpyr.data_ptr(), vpyr.data_ptr(), _stream(dev)),
+                                    _dtype_code(k), kpyr.data_ptr(), vpyr.data_ptr(),
+                                    stream.cuda_stream if stream is not None else _stream(dev)),
           "vb_kv_pyramid")
     return kpyr, vpyr
 
@@ -495,6 +500,31 @@ def ml_attention_bwd(dout, q, kpyr, vpyr, level_mask_u8, out, lse, *, rows=None,
     a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
     check(lib.vb_ml_attn_bwd(ctypes.byref(a), _stream(dev)), "vb_ml_attn_bwd")
     return dq, dk, dv
+
+
+class SideStream:
+    """A second HIP stream per device for work that is independent within one call (the pooled
+    K/V pass beside the mask predictor). ``fork()`` makes it wait for the current stream;
+    ``join()`` makes the current stream wait for it."""
+
+    def __init__(self):
+        self._streams = {}
+
+    def get(self, dev):
+        key = torch.device(dev).index
+        st = self._streams.get(key)
+        if st is None:
+            st = torch.cuda.Stream(device=dev)
+            self._streams[key] = st
+        return st
+
+    def fork(self, dev):
+        st = self.get(dev)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        return st
+
+    def join(self, dev):
+        torch.cuda.current_stream(dev).wait_stream(self.get(dev))
 
 
 def default_scale(D: int) -> float:
