@@ -135,3 +135,21 @@ def test_two_rank_bucketed_all_reduce_equals_single_process():
         a, b = torch.from_numpy(a), torch.from_numpy(b)
         assert torch.equal(a, b)                       # ranks agree exactly
         assert torch.allclose(a, c.detach(), atol=2e-6, rtol=1e-5)
+
+
+def test_qk_dump_counter_and_layout_match_the_reference(tmp_path):
+    """blocksparseattn.py:375-386: timestep = counter % (8*42) // 42, layer = counter % 42;
+    q.pt / k.pt saved at the chosen timesteps under timestep_{t}_layer_{l}/."""
+    from vblade import dump
+    m = dump.QKDumpAttention(str(tmp_path), CpuAttention(), layers=3, steps=4, timesteps=(1, 3))
+    qs = []
+    for c in range(3 * 4 + 2):        # wraps into a second "video"
+        q = torch.full((1, 2, 8, 4), float(c))
+        m(q, q + 0.5, q)
+        qs.append(q)
+    got = dump.load_dumps(str(tmp_path))
+    assert [(t, l) for t, l, _ in got] == [(1, 0), (1, 1), (1, 2), (3, 0), (3, 1), (3, 2)]
+    for t, l, d in got:
+        c = t * 3 + l
+        assert torch.equal(d["q"], qs[c]) and torch.equal(d["k"], qs[c] + 0.5)
+    assert m.counter == 14
