@@ -123,11 +123,11 @@ typedef struct vb_predict_args {
   float energy_threshold;
   int min_keep, max_keep, force_tail;
   void* po;                /* [B,H,nb,nb] storage dtype, contiguous */
-  uint8_t* mask;           /* [B,H,nb,nb] contiguous */
+  uint8_t* mask;           /* [B,H,nb,nb] contiguous, or NULL: scores only (no energy rule) */
   unsigned long long* mask_count; /* nullable */
   int dtype;
   void* workspace;         /* device, 16-byte aligned, >= vb_mask_predict_workspace_size(args) bytes:
-                              the sampled q/k rows staged contiguously */
+                              the sampled k rows staged contiguously and the per-row block maxima */
   uint64_t workspace_bytes;
 } vb_predict_args;
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);

@@ -31,7 +31,7 @@ template <int D> constexpr int kPBufs = 3;
 struct PredParams {
   const void* q; const void* k;
   int64_t qs[3], ks[3];
-  uint8_t* q_s; uint8_t* k_s;   // sampled rows [B,H,nb*32,D] contiguous (workspace)
+  uint8_t* q_s; uint8_t* k_s;   // sampled k rows [B,H,nb*32,D] contiguous (workspace); q_s unused
   uint16_t* rbuf;               // R [B,H,nb(q-block),nb(key block),32 rows] storage bits (workspace)
   const int32_t* rows;
   const int32_t* q_off; const int32_t* k_off;
@@ -163,7 +163,8 @@ __device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int n
   }
 }
 
-// Sampled rows of q and k, gathered once into contiguous [B,H,nb*32,D] (blockIdx.y: 0 = q, 1 = k):
+// Sampled rows of k, gathered once into contiguous [B,H,nb*32,D] (the q fragments are gathered by the
+// predictor's prologue directly, one row per lane):
 // row j*32 + t of (b,h) = reordered position min(j*block + off[b,h,t], L-1) (replicate padding),
 // read at the caller's row rows[pos]. The predictor then streams K by plain LDS-DMA.
 template <class T>
@@ -173,7 +174,7 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nrow = (int64_t)p.nb * 32;
   if (r >= (int64_t)p.B * p.H * nrow) return;
-  const bool isk = blockIdx.y != 0;
+  const bool isk = true;   // q rows are gathered by the predictor itself
   const int jt = r % nrow;
   const int bh = r / nrow;
   const int b = bh / p.H, h = bh % p.H;
@@ -183,7 +184,7 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
   const int64_t* st = isk ? p.ks : p.qs;
   const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(isk ? p.k : p.q) +
                                                     2 * (b * st[0] + h * st[1] + (int64_t)pos * st[2]));
-  u32x4* dst = reinterpret_cast<u32x4*>((isk ? p.k_s : p.q_s) + r * p.D * 2);
+  u32x4* dst = reinterpret_cast<u32x4*>(p.k_s + r * p.D * 2);
   if (CH == 8) {
     u32x4 x[8];
 #pragma unroll
@@ -231,10 +232,13 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   const bool wave_active = qb < nb;
   const int64_t slice = (int64_t)nb * 32 * kRowB;   // bytes of one (b,h) sampled stream
 
-  // Q fragment of this lane's sampled row (B operand of S^T = K_s . Q_s^T)
+  // Q fragment of this lane's sampled row (B operand of S^T = K_s . Q_s^T), gathered straight from
+  // the caller's q: reordered-padded position qb*block + q_off[l32] (replicate padding) at row rows[pos]
   typename T::vec8 qf[KS];
   {
-    const uint8_t* qp = p.q_s + bh * slice + (int64_t)((wave_active ? qb : 0) * 32 + l32) * kRowB;
+    const int b = bh / p.H, h = bh % p.H;
+    const int qrow = sampled_row(wave_active ? qb : 0, p.q_off[(int64_t)bh * 32 + l32], p.block, p.L, p.rows);
+    const uint8_t* qp = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + (int64_t)qrow * p.qs[2]);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
@@ -389,6 +393,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     val[j] = v;
     po[j] = T::from_f32(v);
   }
+  if (p.mask == nullptr) return;   // scores only (the multi-level path ranks them itself)
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
   uint8_t* mrow = p.mask + ((int64_t)bh * nb + qb) * nb;
@@ -452,14 +457,14 @@ static size_t predict_smem_bytes(int nb, int D) {
   return kPWaves * 32 * 4 + (tiles > scratch ? tiles : scratch);
 }
 
-// workspace: sampled q rows | sampled k rows | R
+// workspace: sampled k rows | R
 static uint64_t predict_rows_bytes(int B, int H, int L, int D) {
   const int nb = (L + 127) / 128;
   return (uint64_t)B * H * nb * 32 * D * 2;
 }
 static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
   const uint64_t nb = (L + 127) / 128;
-  return 2 * predict_rows_bytes(B, H, L, D) + (uint64_t)B * H * nb * nb * 32 * 2;
+  return predict_rows_bytes(B, H, L, D) + (uint64_t)B * H * nb * nb * 32 * 2;
 }
 
 template <int D, class T>
@@ -470,7 +475,7 @@ static int launch_predict(const PredParams& p, hipStream_t stream) {
                           (int)smem) != hipSuccess)
     return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
   const int64_t gthreads = (int64_t)p.B * p.H * p.nb * 32;
-  hipLaunchKernelGGL(sample_rows_kernel<T>, dim3((unsigned)((gthreads + 255) / 256), 2), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(sample_rows_kernel<T>, dim3((unsigned)((gthreads + 255) / 256), 1), dim3(256), 0, stream, p);
   if (int rc = check_launch("sample_rows_kernel")) return rc;
   const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
@@ -486,7 +491,7 @@ extern "C" uint64_t vb_mask_predict_workspace_size(const vb_predict_args* a) {
 
 extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   using namespace vb;
-  if (!a || !a->q || !a->k || !a->q_off || !a->k_off || !a->po || !a->mask)
+  if (!a || !a->q || !a->k || !a->q_off || !a->k_off || !a->po)
     return fail(VB_ERR_INVALID, "vb_mask_predict: null argument");
   if (a->B <= 0 || a->H <= 0 || a->L <= 0) return fail(VB_ERR_INVALID, "vb_mask_predict: bad sizes");
   if (a->block != 128 || a->num_keep != 32)
@@ -513,8 +518,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   p.thr = a->energy_threshold;
   p.min_keep = a->min_keep; p.max_keep = a->max_keep; p.force_tail = a->force_tail;
   p.po = a->po; p.mask = a->mask; p.count = a->mask_count;
-  p.q_s = reinterpret_cast<uint8_t*>(a->workspace);
-  p.k_s = p.q_s + rows_b;
+  p.q_s = nullptr;
+  p.k_s = reinterpret_cast<uint8_t*>(a->workspace);
   p.rbuf = reinterpret_cast<uint16_t*>(p.k_s + rows_b);
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);

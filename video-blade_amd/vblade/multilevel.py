@@ -49,7 +49,7 @@ def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=N
     B, H, L, D = q.shape
     if q_off is None or k_off is None:
         q_off, k_off = draw_sample_offsets_qk(B, H, q.device, BLOCK, 32)
-    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, min_keep=1, max_keep=1)
+    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False)
     return po, ops.level_mask(po, mask_ratios)
 
 

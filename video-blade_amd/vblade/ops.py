@@ -282,15 +282,16 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
 # mask predictor, energy rule, pooling, combine
 # ----------------------------------------------------------------------------------------------
 def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_keep=1,
-                 max_keep=1, force_tail=0, scale=None, mask_count=None):
+                 max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True):
     """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
-    po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb]."""
+    po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb] (None with want_mask=False: the scores
+    only, no energy rule)."""
     dev = _require_gpu(q, k, q_off, k_off, rows)
     q, k = _aligned_bhld(q), _aligned_bhld(k)
     B, H, L, D = q.shape
     nb = (L + BLOCK - 1) // BLOCK
     po = torch.empty(B, H, nb, nb, device=dev, dtype=q.dtype)
-    mask = torch.empty(B, H, nb, nb, device=dev, dtype=torch.uint8)
+    mask = torch.empty(B, H, nb, nb, device=dev, dtype=torch.uint8) if want_mask else None
     q_off = q_off.to(torch.int32).contiguous()
     k_off = k_off.to(torch.int32).contiguous()
     a = PredictArgs()
@@ -301,7 +302,7 @@ def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_ke
     a.scale = float(scale) if scale else 0.0
     a.energy_threshold = float(energy_threshold)
     a.min_keep, a.max_keep, a.force_tail = int(min_keep), int(max_keep), int(force_tail)
-    a.po, a.mask, a.mask_count = po.data_ptr(), mask.data_ptr(), _ptr(mask_count)
+    a.po, a.mask, a.mask_count = po.data_ptr(), _ptr(mask), _ptr(mask_count)
     a.dtype = _dtype_code(q)
     lib = _lib.load()
     nbytes = int(lib.vb_mask_predict_workspace_size(ctypes.byref(a)))
