@@ -129,6 +129,9 @@ typedef struct vb_predict_args {
   void* workspace;         /* device, 16-byte aligned, >= vb_mask_predict_workspace_size(args) bytes:
                               the sampled k rows staged contiguously and the per-row block maxima */
   uint64_t workspace_bytes;
+  void* staged_event;      /* nullable hipEvent_t, recorded on `stream` once the sampled rows are
+                              staged (before the score kernel): independent work on another stream
+                              can start then and overlap the score kernel */
 } vb_predict_args;
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);

@@ -468,7 +468,7 @@ static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
 }
 
 template <int D, class T>
-static int launch_predict(const PredParams& p, hipStream_t stream) {
+static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t staged) {
   const size_t smem = predict_smem_bytes(p.nb, D);
   auto kern = mask_predict_kernel<D, T>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -477,6 +477,7 @@ static int launch_predict(const PredParams& p, hipStream_t stream) {
   const int64_t gthreads = (int64_t)p.B * p.H * p.nb * 32;
   hipLaunchKernelGGL(sample_rows_kernel<T>, dim3((unsigned)((gthreads + 255) / 256), 1), dim3(256), 0, stream, p);
   if (int rc = check_launch("sample_rows_kernel")) return rc;
+  if (staged && hipEventRecord(staged, stream) != hipSuccess) return fail(VB_ERR_LAUNCH, "vb_mask_predict: hipEventRecord failed");
   const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
   return check_launch("mask_predict_kernel");
@@ -525,12 +526,13 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);
 #endif
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipEvent_t ev = reinterpret_cast<hipEvent_t>(a->staged_event);
   if (a->dtype == VB_DTYPE_BF16) {
-    if (a->D == 64) return launch_predict<64, BF16>(p, s);
-    if (a->D == 128) return launch_predict<128, BF16>(p, s);
+    if (a->D == 64) return launch_predict<64, BF16>(p, s, ev);
+    if (a->D == 128) return launch_predict<128, BF16>(p, s, ev);
   } else if (a->dtype == VB_DTYPE_F16) {
-    if (a->D == 64) return launch_predict<64, F16>(p, s);
-    if (a->D == 128) return launch_predict<128, F16>(p, s);
+    if (a->D == 64) return launch_predict<64, F16>(p, s, ev);
+    if (a->D == 128) return launch_predict<128, F16>(p, s, ev);
   } else {
     return fail(VB_ERR_INVALID, "vb_mask_predict: unknown dtype");
   }

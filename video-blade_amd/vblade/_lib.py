@@ -53,6 +53,7 @@ class PredictArgs(ctypes.Structure):
         ("po", _vp), ("mask", _vp), ("mask_count", _vp),
         ("dtype", ctypes.c_int),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_uint64),
+        ("staged_event", _vp),
     ]
 
 

@@ -187,7 +187,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
         return getattr(self, "_folded", 0.0) / self.sparsity_counter
 
     # -------------------------------------------------------------------------------- forward
-    def predict_mask(self, q, k, q_off=None, k_off=None, count=None):
+    def predict_mask(self, q, k, q_off=None, k_off=None, count=None, staged_event=None):
         """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores."""
         B, H, L, D = q.shape
         if q_off is None and k_off is None:
@@ -200,7 +200,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
         lo, hi = retain_counts(nb, self.min_retain_ratio, self.max_retain_ratio, self.variant)
         po, mask = ops.mask_predict(q, k, q_off, k_off, rows=self._rows(q.device),
                                     energy_threshold=self.energy_threshold, min_keep=lo,
-                                    max_keep=hi, force_tail=self.force_tail, mask_count=count)
+                                    max_keep=hi, force_tail=self.force_tail, mask_count=count,
+                                    staged_event=staged_event)
         return po, mask
 
     def forward(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *,
@@ -218,17 +219,22 @@ class AdaptiveBlockSparseAttn(nn.Module):
         # predictor (MFMA-bound); they are independent within the call
         fused = not grad and self.combine != "reference"
         pooled = None
-        if fused:
-            # one pass over K/V: pooled K/V + Gilbert-ordered contiguous copies the attention
-            # kernel streams by LDS-DMA (launched first so it runs beside the predictor)
-            side = self._side.fork(q.device) if self.overlap else None
-            pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True, stream=side)
         if block_mask is None:
+            # inference: the pooled K/V pass (one pass over K/V: pooled K/V + the Gilbert-ordered
+            # contiguous copies the attention kernel streams by LDS-DMA; HBM-bound) runs on a side
+            # stream as soon as the predictor has staged its sampled rows, beside the MFMA-bound
+            # score kernel
+            ev = self._side.event(q.device) if (fused and self.overlap) else None
             with torch.no_grad():
-                _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count)
+                _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count, staged_event=ev)
+            if fused:
+                side = self._side.fork(q.device, event=ev) if self.overlap else None
+                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True, stream=side)
         else:
             mask = block_mask.to(torch.uint8)
             count.add_(mask.sum())
+            if fused:
+                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True)
         self._slot_totals.append(B * H * nb * nb)
         self.sparsity_counter += 1
         self.last_mask = mask
@@ -238,7 +244,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
         else:
             # q rows gathered and out rows scattered inside the attention kernel
             kp, vp, k_r, v_r = pooled
-            if self.overlap:
+            if self.overlap and block_mask is None:
                 self._side.join(q.device)
             ev = self.attn_events
             if ev is not None:

@@ -43,13 +43,13 @@ def density(mask_ratios=None) -> float:
     return sum((e - s) / v for v, (s, e) in r.items() if v != 0)
 
 
-def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=None):
+def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=None, staged_event=None):
     """efficient_attn_with_pooling + transfer_attn_to_mask on the (reordered through ``rows``)
     q, k: returns (po [B,H,nb,nb] q.dtype, level mask uint8 [B,H,nb,nb])."""
     B, H, L, D = q.shape
     if q_off is None or k_off is None:
         q_off, k_off = draw_sample_offsets_qk(B, H, q.device, BLOCK, 32)
-    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False)
+    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, staged_event=staged_event)
     return po, ops.level_mask(po, mask_ratios)
 
 
@@ -165,14 +165,16 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
             self.sparsity_counter += 1
             return out
         with torch.no_grad():
-            # the pyramid pass (HBM-bound) on a side stream beside the predictor (MFMA-bound)
-            side = self._side.fork(q.device) if self.overlap else None
-            kpyr, vpyr = ops.kv_pyramid(k, v, rows, stream=side)
+            # the pyramid pass (HBM-bound) on a side stream beside the predictor's score kernel
+            side = None
             if level_mask is None:
+                ev = self._side.event(q.device) if self.overlap else None
                 _, mask = predict_level_mask(q, k, rows=rows, mask_ratios=self.mask_ratios,
-                                             q_off=q_off, k_off=k_off)
+                                             q_off=q_off, k_off=k_off, staged_event=ev)
+                side = self._side.fork(q.device, event=ev) if self.overlap else None
             else:
                 mask = level_mask.to(torch.uint8).contiguous()
+            kpyr, vpyr = ops.kv_pyramid(k, v, rows, stream=side)
             if side is not None:
                 self._side.join(q.device)
             ev = self.attn_events

@@ -282,10 +282,12 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
 # mask predictor, energy rule, pooling, combine
 # ----------------------------------------------------------------------------------------------
 def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_keep=1,
-                 max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True):
+                 max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True,
+                 staged_event=None):
     """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
     po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb] (None with want_mask=False: the scores
-    only, no energy rule)."""
+    only, no energy rule). ``staged_event`` (a torch.cuda.Event) is recorded once the sampled
+    rows are staged, before the score kernel: work waiting on it overlaps the score kernel."""
     dev = _require_gpu(q, k, q_off, k_off, rows)
     q, k = _aligned_bhld(q), _aligned_bhld(k)
     B, H, L, D = q.shape
@@ -308,6 +310,7 @@ def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_ke
     nbytes = int(lib.vb_mask_predict_workspace_size(ctypes.byref(a)))
     ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
     a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
+    a.staged_event = staged_event.cuda_event if staged_event is not None else None
     check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
 
@@ -510,6 +513,18 @@ class SideStream:
 
     def __init__(self):
         self._streams = {}
+        self._events = {}
+
+    def event(self, dev):
+        """A reusable HIP event (created and recorded once so its handle exists) that the
+        library records mid-call (vb_predict_args.staged_event)."""
+        key = torch.device(dev).index
+        ev = self._events.get(key)
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._events[key] = ev
+        return ev
 
     def get(self, dev):
         key = torch.device(dev).index
@@ -519,9 +534,13 @@ class SideStream:
             self._streams[key] = st
         return st
 
-    def fork(self, dev):
+    def fork(self, dev, event=None):
+        """The side stream, made to wait for the current stream (or for ``event`` only)."""
         st = self.get(dev)
-        st.wait_stream(torch.cuda.current_stream(dev))
+        if event is not None:
+            st.wait_event(event)
+        else:
+            st.wait_stream(torch.cuda.current_stream(dev))
         return st
 
     def join(self, dev):
