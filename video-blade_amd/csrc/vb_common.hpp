@@ -80,6 +80,13 @@ __device__ __forceinline__ float add_xor32(float x) {
 
 __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// ---------------------------------------------------------------- HBM passes beside the predictor
+#ifndef VB_POOL_WGS_DEFAULT
+#define VB_POOL_WGS_DEFAULT 0
+#endif
+constexpr int kPoolWgsDefault = VB_POOL_WGS_DEFAULT;
+unsigned pool_grid(int64_t work_items);   // vb_pool.hip
+
 // ---------------------------------------------------------------- host error plumbing
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);

@@ -22,8 +22,8 @@ __global__ void __launch_bounds__(256) kv_pyramid_kernel(const uint8_t* __restri
   constexpr int kCh = D / 8;   // 16-byte chunks per row
   const int ngroups = Lpad / 8;
   const int64_t total = (int64_t)B * H * ngroups * kCh;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= total) return;
+  for (int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+       tid += (int64_t)gridDim.x * blockDim.x) {   // grid-stride (pool_grid)
   const int ch = (int)(tid % kCh);
   const int64_t rest = tid / kCh;
   const int g = (int)(rest % ngroups);
@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(256) kv_pyramid_kernel(const uint8_t* __restri
         *reinterpret_cast<u32x4*>(dst + (int64_t)prow * D * 2) = w;
       }
     }
+  }
   }
 }
 
@@ -143,7 +144,7 @@ extern "C" int vb_kv_pyramid(const void* k, const void* v, const int64_t* k_stri
     return fail(VB_ERR_INVALID, "vb_kv_pyramid: tensors must be 16-byte aligned");
   const int Lpad = (L + 127) / 128 * 128;
   const int64_t total = (int64_t)B * H * (Lpad / 8) * (D / 8);
-  const dim3 grid((unsigned)((total + 255) / 256));
+  const dim3 grid(pool_grid(total));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const uint8_t* kb = static_cast<const uint8_t*>(k);
   const uint8_t* vb_ = static_cast<const uint8_t*>(v);

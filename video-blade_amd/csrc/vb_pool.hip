@@ -2,6 +2,8 @@
 // combine for gfx950: the two HBM-bound element passes of the adaptive path.
 //   simple_pooling (cogvideox/train/special_attentions_local/TrainRelated/cogvideo_blocksparseattn.py:83-88)
 //   + the rearrange gathers (:148-150); the bf16 combine of adaptive_block_sparse_attn (:374-393).
+#include <cstdlib>
+
 #include "vb_common.hpp"
 
 namespace vb {
@@ -16,9 +18,10 @@ __global__ void __launch_bounds__(256) pool_kv_kernel(const uint8_t* k, const ui
                                                       int Lp, uint8_t* kp, uint8_t* vp, uint8_t* k_r,
                                                       uint8_t* v_r) {
   const int CH = D / 8;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)B * H * Lp * CH;
-  if (idx >= total) return;
+  // grid-stride: the launch may use fewer workgroups than chunks (see pool_grid below)
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
   const int ch = idx % CH;
   const int64_t prow = idx / CH;        // (b*H + h)*Lp + pr
   const int pr = prow % Lp;
@@ -55,6 +58,19 @@ __global__ void __launch_bounds__(256) pool_kv_kernel(const uint8_t* k, const ui
   }
   *reinterpret_cast<u32x4*>(kp + (prow * D + ch * 8) * 2) = ok;
   *reinterpret_cast<u32x4*>(vp + (prow * D + ch * 8) * 2) = ov;
+  }
+}
+
+// Workgroups of an HBM-bound pass that runs beside the predictor's score kernel on another stream:
+// a capped, grid-strided launch leaves most CUs to the MFMA-bound kernel instead of flooding the
+// dispatcher (VB_POOL_WGS overrides; 0 = one workgroup per 256 chunks).
+unsigned pool_grid(int64_t work_items) {
+  static const int cap = [] {
+    const char* e = getenv("VB_POOL_WGS");
+    return e ? atoi(e) : kPoolWgsDefault;
+  }();
+  const int64_t n = (work_items + 255) / 256;
+  return (unsigned)((cap > 0 && n > cap) ? cap : n);
 }
 
 // adaptive_block_sparse_attn's combine (cogvideo_blocksparseattn.py:374-393), eager-op rounding
@@ -107,7 +123,7 @@ extern "C" int vb_pool_kv(const void* k, const void* v, const int64_t* k_stride,
     if ((k_stride[i] | v_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_pool_kv: strides must be multiples of 8");
   const int Lp = (L + gap - 1) / gap;
   const int64_t total = (int64_t)B * H * Lp * (D / 8);
-  const dim3 grid((unsigned)((total + 255) / 256));
+  const dim3 grid(pool_grid(total));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   auto* kb = reinterpret_cast<const uint8_t*>(k);
   auto* vb_ = reinterpret_cast<const uint8_t*>(v);
