@@ -26,7 +26,16 @@ constexpr int kMaxNb = 320;        // sampled blocks per side (L <= 40960 at blo
 // keys per LDS tile: D=64 streams four 32-key sampled blocks per barrier (16 MFMAs per wave),
 // D=128 two (also 16 MFMAs); a 3-deep ring keeps the LDS at 48 KiB (3 workgroups per CU)
 template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
-template <int D> constexpr int kPBufs = 3;
+#ifndef VB_PRED_BUFS
+#define VB_PRED_BUFS 3
+#endif
+#ifndef VB_PRED_SPLIT_ENERGY
+#define VB_PRED_SPLIT_ENERGY 0   // 1: the energy rule runs as its own kernel after the scores
+#endif
+#ifndef VB_PRED_MIN_WG
+#define VB_PRED_MIN_WG 2
+#endif
+template <int D> constexpr int kPBufs = VB_PRED_BUFS;
 
 struct PredParams {
   const void* q; const void* k;
@@ -200,8 +209,8 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
   }
 }
 
-template <int D, class T>
-__global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredParams p) {
+template <int D, class T, bool kEnergy>
+__global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel(const PredParams p) {
   constexpr int KS = D / 16;
   constexpr int kRowB = D * 2;                        // bytes per key row
   constexpr int kKT = kKeysPerTile<D> / 32;          // sampled key blocks per tile
@@ -342,11 +351,12 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
     body(t0, std::integral_constant<int, 0>{});
     if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
-    if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
+    if constexpr (kBufs > 2)
+      if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2 % kBufs>{});
     if constexpr (kBufs > 3)
       if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
   }
-  static_assert(kBufs == 3 || kBufs == 4, "the loop body is instantiated once per ring slot");
+  static_assert(kBufs >= 2 && kBufs <= 4, "the loop body is instantiated once per ring slot");
   m = max_xor32(m);   // the two halves saw alternate key blocks
   if (half == 0) mrow_s[wave * 32 + l32] = m;
   __syncthreads();
@@ -393,7 +403,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mask_predict_kernel(const PredPa
     val[j] = v;
     po[j] = T::from_f32(v);
   }
-  if (p.mask == nullptr) return;   // scores only (the multi-level path ranks them itself)
+  if (!kEnergy || p.mask == nullptr) return;   // scores only (energy rule elsewhere / not wanted)
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
   uint8_t* mrow = p.mask + ((int64_t)bh * nb + qb) * nb;
@@ -470,7 +480,7 @@ static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
 template <int D, class T>
 static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t staged) {
   const size_t smem = predict_smem_bytes(p.nb, D);
-  auto kern = mask_predict_kernel<D, T>;
+  auto kern = mask_predict_kernel<D, T, !VB_PRED_SPLIT_ENERGY>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)smem) != hipSuccess)
     return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
@@ -480,7 +490,14 @@ static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t st
   if (staged && hipEventRecord(staged, stream) != hipSuccess) return fail(VB_ERR_LAUNCH, "vb_mask_predict: hipEventRecord failed");
   const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
-  return check_launch("mask_predict_kernel");
+  if (int rc = check_launch("mask_predict_kernel")) return rc;
+  if (VB_PRED_SPLIT_ENERGY && p.mask) {
+    const int rows = p.B * p.H * p.nb;
+    hipLaunchKernelGGL(energy_mask_kernel<T>, dim3((rows + 3) / 4), dim3(256), 0, stream, p.po, rows, p.nb, p.thr,
+                       p.min_keep, p.max_keep, p.force_tail, p.nb, p.mask, p.count);
+    return check_launch("energy_mask_kernel");
+  }
+  return 0;
 }
 
 }  // namespace vb
