@@ -587,16 +587,23 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   if (qvalid) {
     uint8_t* obase = reinterpret_cast<uint8_t*>(p.out) +
                      2 * (b * p.os[0] + h * p.os[1] + (qrow0 + qrow) * p.os[2]);
+    // Each lane holds half of its row's 8-column groups (lane l: columns 8g..8g+3, lane l+32:
+    // 8g+4..8g+7). One v_permlane32_swap per dword pairs groups 2p and 2p+1 so every lane owns 16
+    // contiguous bytes: half the store instructions of the 8-byte form (guide T21).
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * half;
-        u32x2 w;
-        w[0] = pack2<T>(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
-        w[1] = pack2<T>(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
-        if (nan_head) w[0] = w[1] = kNaN2;
-        *reinterpret_cast<u32x2*>(obase + d * 2) = w;
+      for (int pr = 0; pr < 2; ++pr) {
+        u32x2 a, c;
+        a[0] = pack2<T>(o[dt][8 * pr + 0] * inv, o[dt][8 * pr + 1] * inv);
+        a[1] = pack2<T>(o[dt][8 * pr + 2] * inv, o[dt][8 * pr + 3] * inv);
+        c[0] = pack2<T>(o[dt][8 * pr + 4] * inv, o[dt][8 * pr + 5] * inv);
+        c[1] = pack2<T>(o[dt][8 * pr + 6] * inv, o[dt][8 * pr + 7] * inv);
+        if (nan_head) a[0] = a[1] = c[0] = c[1] = kNaN2;
+        const auto sx = __builtin_amdgcn_permlane32_swap(a[0], c[0], false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(a[1], c[1], false, false);
+        const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
+        *reinterpret_cast<u32x4*>(obase + (dt * 32 + 16 * pr + 8 * half) * 2) = w;
       }
     if (p.lse && half == 0) {
       const float v = (m + __log2f(lt)) * kLn2;

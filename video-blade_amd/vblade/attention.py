@@ -225,11 +225,14 @@ class AdaptiveBlockSparseAttn(nn.Module):
             # stream as soon as the predictor has staged its sampled rows, beside the MFMA-bound
             # score kernel
             ev = self._side.event(q.device) if (fused and self.overlap) else None
+            # the side stream's outputs are allocated first: the predictor's temporaries, freed
+            # while its score kernel still runs, must not be recycled into them
+            outs = ops.pool_kv_outputs(k, self.sample_gap, reordered=True) if fused else None
             with torch.no_grad():
                 _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count, staged_event=ev)
             if fused:
                 side = self._side.fork(q.device, event=ev) if self.overlap else None
-                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True, stream=side)
+                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True, stream=side, out=outs)
         else:
             mask = block_mask.to(torch.uint8)
             count.add_(mask.sum())

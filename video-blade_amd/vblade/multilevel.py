@@ -167,6 +167,7 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
         with torch.no_grad():
             # the pyramid pass (HBM-bound) on a side stream beside the predictor's score kernel
             side = None
+            outs = ops.kv_pyramid_outputs(k)   # before the predictor's temporaries (see attention.py)
             if level_mask is None:
                 ev = self._side.event(q.device) if self.overlap else None
                 _, mask = predict_level_mask(q, k, rows=rows, mask_ratios=self.mask_ratios,
@@ -174,7 +175,7 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
                 side = self._side.fork(q.device, event=ev) if self.overlap else None
             else:
                 mask = level_mask.to(torch.uint8).contiguous()
-            kpyr, vpyr = ops.kv_pyramid(k, v, rows, stream=side)
+            kpyr, vpyr = ops.kv_pyramid(k, v, rows, stream=side, out=outs)
             if side is not None:
                 self._side.join(q.device)
             ev = self.attn_events

@@ -344,7 +344,20 @@ def energy_mask(po, *, energy_threshold=0.95, min_keep=1, max_keep=1, force_tail
     return mask
 
 
-def pool_kv(k, v, gap: int, rows=None, reordered: bool = False, stream=None):
+def pool_kv_outputs(k, gap: int, reordered: bool = False):
+    """Allocate pool_kv's outputs (kp, vp[, k_r, v_r]) on the current stream. A caller that launches
+    pool_kv on a side stream allocates them BEFORE enqueueing other work whose temporaries could
+    otherwise be recycled into them while that work still runs."""
+    B, H, L, D = k.shape
+    Lp = (L + gap - 1) // gap
+    kw = dict(device=k.device, dtype=k.dtype)
+    outs = [torch.empty(B, H, Lp, D, **kw), torch.empty(B, H, Lp, D, **kw)]
+    if reordered:
+        outs += [torch.empty(B, H, L, D, **kw), torch.empty(B, H, L, D, **kw)]
+    return tuple(outs)
+
+
+def pool_kv(k, v, gap: int, rows=None, reordered: bool = False, stream=None, out=None):
     """vb_pool_kv: mean over `gap` consecutive reordered tokens (replicate pad) -> kp, vp; with
     reordered=True also returns the Gilbert-ordered contiguous copies (k_r, v_r) written in the
     same pass. ``stream`` (a torch.cuda.Stream) launches there instead of the current stream; the
@@ -352,12 +365,15 @@ def pool_kv(k, v, gap: int, rows=None, reordered: bool = False, stream=None):
     using them."""
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
+    if stream is not None:   # read (and written) on the side stream: no reuse before it is done
+        for t in (k, v, rows) + tuple(out or ()):
+            if t is not None:
+                t.record_stream(stream)
     B, H, L, D = k.shape
-    Lp = (L + gap - 1) // gap
-    kp = torch.empty(B, H, Lp, D, device=dev, dtype=k.dtype)
-    vp = torch.empty(B, H, Lp, D, device=dev, dtype=v.dtype)
-    k_r = torch.empty(B, H, L, D, device=dev, dtype=k.dtype) if reordered else None
-    v_r = torch.empty(B, H, L, D, device=dev, dtype=v.dtype) if reordered else None
+    if out is None:
+        out = pool_kv_outputs(k, gap, reordered)
+    kp, vp = out[0], out[1]
+    k_r, v_r = (out[2], out[3]) if reordered else (None, None)
     check(_lib.load().vb_pool_kv(k.data_ptr(), v.data_ptr(), ctypes.cast(_s3(k), ctypes.c_void_p),
                                  ctypes.cast(_s3(v), ctypes.c_void_p), _ptr(rows), B, H, L, D,
                                  int(gap), _dtype_code(k), kp.data_ptr(), vp.data_ptr(),
@@ -394,16 +410,26 @@ def kv_pyramid_rows(L: int) -> int:
     return int(_lib.load().vb_kv_pyramid_rows(int(L)))
 
 
-def kv_pyramid(k, v, rows=None, stream=None):
+def kv_pyramid_outputs(k):
+    """Allocate kv_pyramid's outputs on the current stream (see pool_kv_outputs)."""
+    B, H, L, D = k.shape
+    R = kv_pyramid_rows(L)
+    return (torch.empty(B, H, R, D, device=k.device, dtype=k.dtype),
+            torch.empty(B, H, R, D, device=k.device, dtype=k.dtype))
+
+
+def kv_pyramid(k, v, rows=None, stream=None, out=None):
     """vb_kv_pyramid: K/V [B,H,L,D] (reordered through `rows`) -> pyramids [B,H,15*Lpad/8,D]:
     level-1 rows (zero beyond L), then the 2x, 4x, 8x mean-pooled rows (replicate padding).
     ``stream``: as pool_kv."""
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
+    if stream is not None:   # see pool_kv
+        for t in (k, v, rows) + tuple(out or ()):
+            if t is not None:
+                t.record_stream(stream)
     B, H, L, D = k.shape
-    R = kv_pyramid_rows(L)
-    kpyr = torch.empty(B, H, R, D, device=dev, dtype=k.dtype)
-    vpyr = torch.empty(B, H, R, D, device=dev, dtype=v.dtype)
+    kpyr, vpyr = out if out is not None else kv_pyramid_outputs(k)
     check(_lib.load().vb_kv_pyramid(k.data_ptr(), v.data_ptr(), ctypes.cast(_s3(k), ctypes.c_void_p),
                                     ctypes.cast(_s3(v), ctypes.c_void_p), _ptr(rows), B, H, L, D,
                                     _dtype_code(k), kpyr.data_ptr(), vpyr.data_ptr(),
