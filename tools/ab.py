@@ -60,6 +60,18 @@ def main():
                                            heavy_rows=m.force_tail)
         elif a.what == "pred":
             fn = lambda: m.predict_mask(q, k, qo, ko)  # noqa
+        elif a.what == "bwd":   # the training-path backward (vb_attn_bwd) on the two-branch forward
+            do = torch.randn_like(q)
+            gap = m.sample_gap
+            out1, lse1 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,
+                                           heavy_rows=m.force_tail)
+            out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
+                                           need_lse=True)
+            _, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
+            fn = lambda: ops.attention_bwd(do, q, k_r, v_r, out1, lse1, block_mask=mask, q_rows=rows,  # noqa
+                                           kv_rows=rows, kp=kp, vp=vp, out2=out2, lse2=lse2,
+                                           alpha=alpha, gap=gap, heavy_rows=m.force_tail)[0]
+            fl = 2.5 * fl
         else:
             fn = lambda: m(q, k, v)  # noqa
         ref = None
@@ -69,7 +81,7 @@ def main():
                 _lib._lib = libs[t]
                 out = fn()
                 torch.cuda.synchronize()
-                if a.what == "attn":
+                if a.what in ("attn", "bwd"):
                     if ref is None:
                         ref = out.float()
                     else:
@@ -88,7 +100,7 @@ def main():
         base = statistics.median(times[keys[0]])
         for kk, t in zip(keys, a.tags):
             md = statistics.median(times[kk])
-            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what == "attn" else ""
+            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what in ("attn", "bwd") else ""
             print(f"{variant} {a.what} {kk}: median {md:.4f} ms (min {min(times[kk]):.4f}){extra}  "
                   f"x{base / md:.3f} vs {a.tags[0]}", flush=True)
 

@@ -383,21 +383,38 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
           dp[r] = pr * (dp[r] - Dv[e]);
         }
       }
+      // dV^T += dO^T.P and dK^T += Q^T.dS over (16-row half sb, 32-wide d tile dt) steps; the four
+      // transposed reads of step j+1 are issued before step j's MFMAs and waited for with
+      // lgkmcnt(4), so each wait only covers reads issued one step earlier
+      typename T::vec8 pp[2], pd[2];
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
-        const typename T::vec8 pp = pack8<T>(s, 8 * sb);
-        const typename T::vec8 pd = pack8<T>(dp, 8 * sb);
-        const int rr = 32 * u + 16 * sb + trr;
+        pp[sb] = pack8<T>(s, 8 * sb);
+        pd[sb] = pack8<T>(dp, 8 * sb);
+      }
+      constexpr int NST = 2 * DT;
+      s16x4 rdo[2][2], rq[2][2];   // [ring][lo/hi]
+      auto rd = [&](int j, int slot) __attribute__((always_inline)) {
+        const int rr = 32 * u + 16 * (j / DT) + trr;
+        const int cc = 32 * (j % DT) + trc;
+        rdo[slot][0] = lds_tr4_asm_at(dot, dual_off_col<D>(rr, cc));
+        rdo[slot][1] = lds_tr4_asm_at(dot, dual_off_col<D>(rr + 8, cc));
+        rq[slot][0] = lds_tr4_asm_at(qt, dual_off_col<D>(rr, cc));
+        rq[slot][1] = lds_tr4_asm_at(qt, dual_off_col<D>(rr + 8, cc));
+      };
+      rd(0, 0);
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          s16x4 dol = lds_tr4_asm_at(dot, dual_off_col<D>(rr, 32 * dt + trc));
-          s16x4 doh = lds_tr4_asm_at(dot, dual_off_col<D>(rr + 8, 32 * dt + trc));
-          s16x4 ql = lds_tr4_asm_at(qt, dual_off_col<D>(rr, 32 * dt + trc));
-          s16x4 qh = lds_tr4_asm_at(qt, dual_off_col<D>(rr + 8, 32 * dt + trc));
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(dol), "+v"(doh), "+v"(ql), "+v"(qh));
-          dv[dt] = T::mfma32(join8<T>(dol, doh), pp, dv[dt]);
-          dk[dt] = T::mfma32(join8<T>(ql, qh), pd, dk[dt]);
+      for (int j = 0; j < NST; ++j) {
+        const int sl = j & 1;
+        if (j + 1 < NST) {
+          rd(j + 1, sl ^ 1);
+          asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(rdo[sl][0]), "+v"(rdo[sl][1]), "+v"(rq[sl][0]), "+v"(rq[sl][1]));
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rdo[sl][0]), "+v"(rdo[sl][1]), "+v"(rq[sl][0]), "+v"(rq[sl][1]));
         }
+        const int sb = j / DT, dt = j % DT;
+        dv[dt] = T::mfma32(join8<T>(rdo[sl][0], rdo[sl][1]), pp[sb], dv[dt]);
+        dk[dt] = T::mfma32(join8<T>(rq[sl][0], rq[sl][1]), pd[sb], dk[dt]);
       }
     }
     __builtin_amdgcn_s_barrier();  // buffer t & 1 is free for tile t + 2
@@ -797,17 +814,29 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
           dp[r] = pr * (dp[r] - Dr);
         }
       }
+      // dQ^T += K^T.dS^T over (16-key half sb, d tile dt) steps, reads one step ahead (lgkmcnt(2))
+      typename T::vec8 pdv[2];
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        const typename T::vec8 pd = pack8<T>(dp, 8 * sb);
-        const int rr = kt * 32 + 16 * sb + trr;
+      for (int sb = 0; sb < 2; ++sb) pdv[sb] = pack8<T>(dp, 8 * sb);
+      constexpr int NST = 2 * DT;
+      s16x4 rk[2][2];
+      auto rd = [&](int j, int slot) __attribute__((always_inline)) {
+        const int rr = kt * 32 + 16 * (j / DT) + trr;
+        const int cc = 32 * (j % DT) + trc;
+        rk[slot][0] = lds_tr4_asm_at(kt_, dual_off_col<D>(rr, cc));
+        rk[slot][1] = lds_tr4_asm_at(kt_, dual_off_col<D>(rr + 8, cc));
+      };
+      rd(0, 0);
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          s16x4 lo = lds_tr4_asm_at(kt_, dual_off_col<D>(rr, 32 * dt + trc));
-          s16x4 hi = lds_tr4_asm_at(kt_, dual_off_col<D>(rr + 8, 32 * dt + trc));
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi));
-          dq[dt] = T::mfma32(join8<T>(lo, hi), pd, dq[dt]);
+      for (int j = 0; j < NST; ++j) {
+        const int sl = j & 1;
+        if (j + 1 < NST) {
+          rd(j + 1, sl ^ 1);
+          asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(rk[sl][0]), "+v"(rk[sl][1]));
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rk[sl][0]), "+v"(rk[sl][1]));
         }
+        dq[j % DT] = T::mfma32(join8<T>(rk[sl][0], rk[sl][1]), pdv[j / DT], dq[j % DT]);
       }
     }
     __builtin_amdgcn_s_barrier();
