@@ -31,6 +31,7 @@
 // No atomics: every gradient element is written by exactly one workgroup, so results are
 // bit-reproducible run to run (the reference's deterministic=True).
 #include <cstdlib>
+#include <type_traits>
 
 #include "vb_tiles.hpp"
 
@@ -184,10 +185,11 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
   constexpr int kCh = RB / 16;
   constexpr int kInst = 2 * kInstTile + 1;  // Q, dO, stats (1 KiB)
   constexpr int kBufBytes = 2 * kTileBytes + 1024;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBufBytes + kMaxBlocks * 3 + 16];
-  uint16_t* list = reinterpret_cast<uint16_t*>(smem + 2 * kBufBytes);
-  int* list_n = reinterpret_cast<int*>(smem + 2 * kBufBytes + kMaxBlocks * 2);
-  uint8_t* list_bits = smem + 2 * kBufBytes + kMaxBlocks * 2 + 16;   // multi-level: active blocks
+  constexpr int kBufs = 3;                   // LDS ring: tile t read, t+1 in flight, t+2 being issued
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kBufs * kBufBytes + kMaxBlocks * 3 + 16];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
+  int* list_n = reinterpret_cast<int*>(smem + kBufs * kBufBytes + kMaxBlocks * 2);
+  uint8_t* list_bits = smem + kBufs * kBufBytes + kMaxBlocks * 2 + 16;   // multi-level: active blocks
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -305,29 +307,41 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 
   const uint8_t* qsrc = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + qrow0 * p.qs[2]);
   const uint8_t* dosrc = reinterpret_cast<const uint8_t*>(p.dout) + 2 * (b * p.dos[0] + h * p.dos[1] + qrow0 * p.dos[2]);
-  const int64_t qstride = 2 * p.qs[2], dostride = 2 * p.dos[2];
+  const int qrowb = 2 * (int)p.qs[2], dorowb = 2 * (int)p.dos[2];   // host: every slice < 2 GiB
   const float* stsrc = p.stats + (int64_t)bh * p.ntile * 256;
 
-  // DMA of tile t (64 q rows) into buffer t & 1: instruction i -> Q (i < kInstTile), dO, stats.
-  auto issue = [&](int t) __attribute__((always_inline)) {
+  // Tile t (64 q rows) -> ring slot t % kBufs by LDS-DMA through buffer descriptors: this wave
+  // issues instructions i = wave + 4k (i < kInstTile: Q, then dO, then the stats KiB). A lane's
+  // part of each instruction (row within the tile, swizzled chunk) is a fixed voffset; the tile's
+  // first row is the scalar soffset. Rows past Lq read as zeros (their stats make P = 0).
+  constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
+  const bool many = wave < (kInst & 3);
+  const srd_t q_srd = make_srd(qsrc, (int)((int64_t)(Lq - 1) * qrowb + RB));
+  const srd_t do_srd = make_srd(dosrc, (int)((int64_t)(Lq - 1) * dorowb + RB));
+  const srd_t st_srd = make_srd(stsrc, p.ntile * 1024);
+  int voff[kHi];
+#pragma unroll
+  for (int k = 0; k < kHi; ++k) {
+    const int i = wave + 4 * k;
+    voff[k] = lane * 16;
+    if (i < 2 * kInstTile) {
+      const int ii = i < kInstTile ? i : i - kInstTile;
+      const int r = ii * kRowsPerInst + lane / kCh;
+      const int c = (lane % kCh) ^ dual_swz<D>(r);
+      voff[k] = r * (i < kInstTile ? qrowb : dorowb) + c * 16;
+    }
+  }
+  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
     const int qb = __builtin_amdgcn_readfirstlane(list[t >> 1]);
     const int row0 = qb * kBlk + (t & 1) * kT;
-    const int nvalid = min(kT, Lq - row0);
-    uint8_t* buf = smem + (t & 1) * kBufBytes;
-    for (int i = wave; i < kInst; i += 4) {
-      const void* src;
-      if (i < 2 * kInstTile) {
-        const int ii = i < kInstTile ? i : i - kInstTile;
-        const int r = ii * kRowsPerInst + lane / kCh;
-        const int c = (lane % kCh) ^ dual_swz<D>(r);
-        const int sr = row0 + min(r, nvalid - 1);
-        src = i < kInstTile ? (const void*)(qsrc + sr * qstride + c * 16)
-                            : (const void*)(dosrc + sr * dostride + c * 16);
-      } else {
-        src = stsrc + (row0 / 64) * 256 + lane * 4;
-      }
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+    uint8_t* buf = smem + slot * kBufBytes;
+#pragma unroll
+    for (int k = 0; k < kHi; ++k) {
+      const int i = wave + 4 * k;
+      if (i >= kInst) break;
+      if (i < kInstTile) dma16(q_srd, buf + i * 1024, voff[k], row0 * qrowb);
+      else if (i < 2 * kInstTile) dma16(do_srd, buf + i * 1024, voff[k], row0 * dorowb);
+      else dma16(st_srd, buf + i * 1024, voff[k], (row0 / 64) * 1024);
     }
   };
 
@@ -339,20 +353,23 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 
   const int trr = tr_row(lane), trc = tr_col(lane);
   constexpr int fL = (kPooled && !kML) ? 2 : 0;  // stats fields of this branch
-  constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
-  const bool many = wave < (kInst & 3);
 
-  if (ntiles > 0) issue(0);
-  for (int t = 0; t < ntiles; ++t) {
+  if (ntiles > 0) issue(0, 0);
+  if (ntiles > 1) issue(1, 1);
+  // The loop body is instantiated once per ring slot: every LDS address is a compile-time offset.
+  auto body = [&](int t, auto U) __attribute__((always_inline)) {
+    constexpr int u_slot = decltype(U)::value;
+    // retire this wave's DMAs of tile t (tile t+1 stays in flight); the barrier makes every wave's
+    // part visible and proves slot (t-1) % kBufs is no longer being read
     if (t + 1 < ntiles) {
-      issue(t + 1);
       if (many) VB_WAIT_VMCNT(kHi);
       else VB_WAIT_VMCNT(kLo);
     } else {
       VB_WAIT_VMCNT(0);
     }
     __builtin_amdgcn_s_barrier();
-    const uint8_t* qt = smem + (t & 1) * kBufBytes;
+    if (t + 2 < ntiles) issue(t + 2, (u_slot + 2) % kBufs);
+    const uint8_t* qt = smem + u_slot * kBufBytes;
     const uint8_t* dot = qt + kTileBytes;
     const float* st = reinterpret_cast<const float*>(qt + 2 * kTileBytes);
     // multi-level pooled items: keys of blocks without level 2^e for this q-block take no part
@@ -417,7 +434,11 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
         dk[dt] = T::mfma32(join8<T>(rq[sl][0], rq[sl][1]), pd[sb], dk[dt]);
       }
     }
-    __builtin_amdgcn_s_barrier();  // buffer t & 1 is free for tile t + 2
+  };
+  for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
+    body(t0, std::integral_constant<int, 0>{});
+    if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
+    if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
   }
 
   // ---- epilogue: lane = key, registers = d ---------------------------------------------------------
@@ -958,6 +979,10 @@ static WsLayout ws_layout(int B, int H, int Lq, int D, bool copies, int Lkp) {
 }
 
 static bool mul8(const int64_t* s) { return ((s[0] | s[1] | s[2]) & 7) == 0; }
+// one (b,h) slice of L rows at `row_stride` elements must be addressable by a 32-bit buffer offset
+static bool slice_ok(int L, int64_t row_stride, int D) {
+  return (int64_t)(L - 1) * 2 * row_stride + 2 * D < (int64_t(1) << 31);
+}
 static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace vb
@@ -999,6 +1024,8 @@ extern "C" int vb_attn_bwd(const vb_attn_bwd_args* a, void* stream) {
   const WsLayout w = ws_layout(a->B, a->H, a->Lq, a->D, a->q_rows != nullptr, pool ? a->Lkp : 0);
   if (!a->workspace || a->workspace_bytes < w.total || !al16(a->workspace))
     return fail(VB_ERR_INVALID, "vb_attn_bwd: workspace missing or smaller than vb_attn_bwd_workspace_size()");
+  if (!a->q_rows && (!slice_ok(a->Lq, a->q_stride[2], a->D) || !slice_ok(a->Lq, a->dout_stride[2], a->D)))
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_bwd: a q/dout (b,h) slice spans >= 2 GiB");
   uint8_t* ws = reinterpret_cast<uint8_t*>(a->workspace);
 
   PrepParams pp{};
@@ -1083,6 +1110,8 @@ extern "C" int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, c
   const WsLayout w = ws_layout(batch, num_heads, max_seqlen_q, head_dim, false, 0);
   if (!workspace || workspace_bytes < w.total || !al16(workspace))
     return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: workspace missing or too small");
+  if (!slice_ok(max_seqlen_q, (int64_t)num_heads * head_dim, head_dim))
+    return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: a sequence's q/dout span >= 2 GiB");
   const void* ptrs[] = {dout, q_unpad, k_unpad, v_unpad, out_unpad, dq, dk, dv};
   for (const void* q : ptrs)
     if (!al16(q)) return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: tensors must be 16-byte aligned");
@@ -1176,6 +1205,8 @@ extern "C" int vb_ml_attn_bwd(const vb_ml_attn_bwd_args* a, void* stream) {
   const MlWs w = ml_ws_layout(a->B, a->H, a->L, a->D, a->rows != nullptr);
   if (!a->workspace || a->workspace_bytes < w.total || !al16(a->workspace))
     return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: workspace missing or smaller than vb_ml_attn_bwd_workspace_size()");
+  if (!a->rows && (!slice_ok(a->L, a->q_stride[2], a->D) || !slice_ok(a->L, a->dout_stride[2], a->D)))
+    return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_bwd: a q/dout (b,h) slice spans >= 2 GiB");
   uint8_t* ws = reinterpret_cast<uint8_t*>(a->workspace);
   const int Lpad = nb * 128;
   const int R = 15 * (Lpad / 8);
