@@ -99,6 +99,30 @@ def test_online_softmax_rescale_branch_is_exercised():
     assert (out.float().cpu() - ref).abs().max() <= 2.5e-2
 
 
+@pytest.mark.parametrize("D", [64, 128])
+def test_huge_late_scores_rescale_both_kernels(D):
+    """Scores ~100-300 log2-units above the first tile's max (keys = 6-20 x a query) in the first
+    and second 32-key half of a tile, in the tail tile and for several queries of one wave.
+    need_lse=True runs the training kernel (unscaled Q): exact to bf16 rounding. The inference
+    kernel (kCBias: Q pre-scaled by scale*log2(e) and rounded to bf16) is checked against the
+    oracle run on that same pre-scaled query, and against the exact oracle by PSNR: with keys of
+    this norm the pre-scale rounding alone moves outputs by ~3 bf16 ulps."""
+    L = 700
+    q, k, v = (_rand(1, 1, L, D, seed=40 + s) for s in range(3))
+    for qi, ki, mult in ((5, 650, 12.0), (6, 300, 12.0), (7, 690, 14.0), (40, 70, 12.0),
+                         (41, 200, 6.0), (130, 10, 20.0)):
+        k[0, 0, ki] = q[0, 0, qi] * mult
+    ref, _ = O.block_sparse_attention(q, k, v, None)
+    out_t, _ = _ops().attention_fwd(q.to(DEV), k.to(DEV), v.to(DEV), need_lse=True)
+    assert (out_t.float().cpu() - ref).abs().max() <= 2.5e-2
+    out = _ops().attention_fwd(q.to(DEV), k.to(DEV), v.to(DEV)).float().cpu()
+    assert torch.isfinite(out).all()
+    qs = (q.float() * (D ** -0.5 * 1.4426950408889634)).to(q.dtype)
+    ref_s, _ = O.block_sparse_attention(qs, k, v, None, sm_scale=math.log(2.0))
+    assert (out - ref_s).abs().max() <= 2.5e-2
+    assert psnr(out, ref) >= 40
+
+
 def test_row_index_gather_scatter_equals_permuted_oracle():
     B, H, L, D = 1, 2, 900, 64
     q, k, v = (_rand(B, H, L, D, seed=30 + s) for s in range(3))

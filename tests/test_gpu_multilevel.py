@@ -314,7 +314,9 @@ def test_ml_backward_deterministic_and_module_autograd():
         grads.append((qq.grad, kk.grad, vv.grad))
     for a, b in zip(*grads):
         assert torch.equal(a, b)
-    # the inference path gives the same output as the autograd op
+    # the inference path gives the autograd op's output up to the inference kernel's extra
+    # rounding of q * scale * log2(e) to bf16 (vb_attn_fwd.hip, kCBias)
     with torch.no_grad():
         out_inf = mod(q, k, v, level_mask=mask)
-    assert torch.equal(out_inf, out.detach())
+    assert (out_inf.float() - out.detach().float()).abs().max().item() <= 2.5e-2
+    assert _rel(out_inf.float().cpu(), out.detach().float().cpu()) <= 5e-3

@@ -43,11 +43,16 @@ __device__ __forceinline__ unsigned long long vb_stamp() {
 #define VB_ACC(i, d)
 #endif
 
-template <int D, class T, bool kPool, bool kKvRows, bool kML = false>
+template <int D, class T, bool kPool, bool kKvRows, bool kML = false, bool kCBias = false>
 __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) attn_fwd_kernel(const FwdParams p) {
   constexpr int KS = D / 16;                   // k-steps of the QK^T product
   constexpr int DT = D / 32;                   // 32-wide d tiles of the output
   constexpr bool kSplitPV = VB_FWD_SPLIT_PV && D == 64;   // measured: +0.8 % at D=64, -1.4 % at D=128
+  // kCBias (inference launches: no LSE output): the S accumulator starts at (bias - m) instead of 0
+  // and Q is pre-scaled by scale*log2(e), so every score leaves the MFMA as the exp2 argument itself:
+  // no per-score v_fma before the v_exp (the D=64 loop is VALU-issue-bound). The extra rounding of
+  // q*scale to 16 bits stays within the stated tolerance; launches that return the LSE for a
+  // backward keep the unscaled Q so forward and backward see the same scores.
   constexpr int kRowB = D * 2;                 // bytes per key row
   constexpr int kMatBytes = kKT * kRowB;       // one 64-key K (or V) tile
   constexpr int kBufBytes = 2 * kMatBytes;     // K image then V image
@@ -168,6 +173,14 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
+    if constexpr (kCBias) {
+      // scores in the exp2 domain straight out of the MFMA: Q carries the softmax scale * log2(e)
+      // (one extra rounding of q to the storage type; the stated tolerance covers it)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[s][e] = T::from_f32(T::to_f32(qf[s][e]) * p.c);
+    }
     // Launder the Q fragment through an empty asm: the loop's MFMAs then depend on the asm, not
     // on the global loads, so hipcc's waitcnt pass does not count them against the DMA ring.
 #pragma unroll
@@ -348,8 +361,15 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   for (int i = 0; i < DT; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-  float m = -INFINITY;  // running max (exp2 domain) of this lane's query row
+  float m = kCBias ? 0.f : -INFINITY;  // running max (exp2 domain) of this lane's query row
   float l = 0.f;        // running partial row sum (this half's keys)
+  // kCBias: cb = cur_bias - m in every register (the first QK^T MFMA's C operand); `first` forces
+  // the first tile to set m from its own maximum
+  f32x16 cb;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) cb[r] = 0.f;
+  float cur_bias = 0.f;
+  bool first = true;
 #if VB_MFMA_ROWSUM
   // Row sums on the matrix core (D=64 is VALU-bound): lsum += ones . P^T, every register of the
   // accumulator = the lane's full row sum of the bf16 P that also feeds O (no VALU adds).
@@ -385,15 +405,29 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     constexpr int kSlot = decltype(U)::value;
     const uint8_t* kl = smem + kSlot * kBufBytes;
     f32x16 s[2];
+    if constexpr (kCBias) {
+      if (bias != cur_bias) {   // wave-uniform; only where the tile source changes (pooled, levels)
+        asm volatile("");
+        const float db = bias - cur_bias;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cb[r] += db;
+        cur_bias = bias;
+      }
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       typename T::vec8 kf[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(kl + kt * 32 * kRowB, k_lane[ks]);
+      if constexpr (kCBias) {
+        s[kt] = T::mfma32(kf[0], qf[0], cb);
+      } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
+        for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
+        s[kt] = T::mfma32(kf[0], qf[0], s[kt]);
+      }
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s[kt] = T::mfma32(kf[ks], qf[ks], s[kt]);
+      for (int ks = 1; ks < KS; ++ks) s[kt] = T::mfma32(kf[ks], qf[ks], s[kt]);
     }
     // V^T fragments (ds_read_b64_tr_b16) for the first VPRE k-steps, issued before the softmax
     // VALU so they land while it runs; the rest are fetched one k-step ahead inside the PV loop.
@@ -434,13 +468,38 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     const float f1 = max3f(mq[0], mq[1], s[0][7]);
     const float f2 = max3f(mq[2], mq[3], s[0][15]);
     float mt = max3f(max3f(f1, f2, s[1][7]), s[1][15], s[1][15]);
-    mt = max_xor32(mt) * p.c + bias;            // tile row max, exp2 domain
+    if constexpr (kCBias) mt = max_xor32(mt);  // tile row max relative to m (bias included)
+    else mt = max_xor32(mt) * p.c + bias;       // tile row max, exp2 domain
     // Deferred rescale (guide T13): the running max m is raised only when some row's tile max
     // exceeds it by more than kRescaleSlack (log2 units), so P = exp2(s - m) <= 2^kRescaleSlack.
     // O and l always share the same m, so the result is exact up to rounding; without the slack
     // nearly every tile of a 32-row wave rescales (some row's max grows), a 40-VALU O-wide pass.
     // The empty volatile asm keeps hipcc from if-converting this block into every iteration.
-    if (!__all(mt <= m + kRescaleSlack)) {
+    if (kCBias) {
+      if (first || !__all(mt <= kRescaleSlack)) {
+        asm volatile("");
+        // first tile: m := the tile's max (O and l are still zero; alpha would be meaningless)
+        const float delta = first ? mt : fmaxf(mt, 0.f);
+        const float alpha = first ? 0.f : exp2_fast(-delta);
+        m += delta;
+        l *= alpha;
+#if VB_MFMA_ROWSUM
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lsum[r] *= alpha;
+#endif
+#pragma unroll
+        for (int i = 0; i < DT; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[kt][r] -= delta;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cb[r] -= delta;
+        first = false;
+      }
+    } else if (!__all(mt <= m + kRescaleSlack)) {
       asm volatile("");
       const float mn = fmaxf(m, mt);
       const float alpha = exp2_fast(m - mn);
@@ -462,7 +521,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = fmaf(s[kt][r], p.c, nbias);
+          const float e = kCBias ? s[kt][r] : fmaf(s[kt][r], p.c, nbias);
           s[kt][r] = e;
           ls += e;
         }
@@ -470,7 +529,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[kt][r] = exp2_fast(fmaf(s[kt][r], p.c, nbias));
+        for (int r = 0; r < 16; ++r) s[kt][r] = exp2_fast(kCBias ? s[kt][r] : fmaf(s[kt][r], p.c, nbias));
     } else if (kSplitPV) {
       // exp of the first 32 keys, their P.V k-steps, then the second 32: the PV MFMAs of the first
       // half overlap the second half's exp VALU (same sums, same order: bit-identical results)
@@ -479,7 +538,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = exp2_fast(fmaf(s[kt][r], p.c, nbias));
+          const float e = exp2_fast(kCBias ? s[kt][r] : fmaf(s[kt][r], p.c, nbias));
           s[kt][r] = e;
           lq[(2 * kt + r) & 3] += e;
         }
@@ -499,7 +558,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = exp2_fast(fmaf(s[kt][r], p.c, nbias));
+          const float e = exp2_fast(kCBias ? s[kt][r] : fmaf(s[kt][r], p.c, nbias));
           s[kt][r] = e;
           lq[(2 * kt + r) & 3] += e;
         }
@@ -642,7 +701,12 @@ template <int D, class T>
 static int launch_fwd(const FwdParams& p, bool pool, hipStream_t stream) {
   const dim3 grid(p.nbq * p.B * p.H);
   const bool rows = p.kv_rows != nullptr;
-  if (pool && rows)
+  const bool cbias = VB_FWD_CBIAS && p.lse == nullptr && !rows;
+  if (cbias && pool)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, false, false, true>), grid, dim3(kThreads), 0, stream, p);
+  else if (cbias)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, false, false, true>), grid, dim3(kThreads), 0, stream, p);
+  else if (pool && rows)
     hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, true>), grid, dim3(kThreads), 0, stream, p);
   else if (pool)
     hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, false>), grid, dim3(kThreads), 0, stream, p);
@@ -774,11 +838,16 @@ extern "C" int vb_ml_attn_fwd(const vb_ml_attn_args* a, void* stream) {
   p.heavy_rows = a->heavy_rows;
   const dim3 grid(p.nbq * p.B * p.H);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool cb = VB_FWD_CBIAS && p.lse == nullptr;   // inference launches (see kCBias)
   if (a->dtype == VB_DTYPE_BF16) {
-    if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, BF16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+    if (a->D == 64 && cb) hipLaunchKernelGGL((attn_fwd_kernel<64, BF16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
+    else if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, BF16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+    else if (cb) hipLaunchKernelGGL((attn_fwd_kernel<128, BF16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
     else hipLaunchKernelGGL((attn_fwd_kernel<128, BF16, false, false, true>), grid, dim3(kThreads), 0, st, p);
   } else if (a->dtype == VB_DTYPE_F16) {
-    if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, F16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+    if (a->D == 64 && cb) hipLaunchKernelGGL((attn_fwd_kernel<64, F16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
+    else if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, F16, false, false, true>), grid, dim3(kThreads), 0, st, p);
+    else if (cb) hipLaunchKernelGGL((attn_fwd_kernel<128, F16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
     else hipLaunchKernelGGL((attn_fwd_kernel<128, F16, false, false, true>), grid, dim3(kThreads), 0, st, p);
   } else {
     return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: unknown dtype");

@@ -37,6 +37,9 @@ struct FwdParams {
 #ifndef VB_FWD_SPLIT_PV
 #define VB_FWD_SPLIT_PV 1   // D=64: P.V of the first 32 keys issued before the exp of the second 32
 #endif
+#ifndef VB_FWD_CBIAS
+#define VB_FWD_CBIAS 1      // S accumulator seeded with (bias - m), Q pre-scaled: no per-score fma
+#endif
 #ifndef VB_FWD_WAVES_D64
 #define VB_FWD_WAVES_D64 3  // waves per SIMD the D=64 kernel is register-budgeted for
 #endif
