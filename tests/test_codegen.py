@@ -1,0 +1,56 @@
+"""Code-generation guards for the attention forward (CPU: hipcc cross-compiles gfx950).
+
+The D=64 forward runs at the 168-VGPR budget of 3 waves per SIMD. When the register allocator
+spills a loop-invariant DMA offset, the reload (a scratch load) sits in the tile-issue block and
+hipcc puts `s_waitcnt vmcnt(0)` in front of the DMA that uses it: that drains the whole LDS-DMA
+ring on every tile (measured 20 % slower). These tests fail the build instead."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "video-blade_amd", "csrc", "vb_attn_fwd.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+# the product launches: <D, BF16, pooled, no kv_rows, not multi-level, kCBias> and the LSE launch
+KERNELS = [
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb1EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb1EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb0EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb0EEEvNS_9FwdParamsE",
+]
+
+
+@pytest.fixture(scope="module")
+def fwd_asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("asm") / "fwd.s"
+    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "video-blade_amd", "csrc"),
+           "-fno-slp-vectorize", "-fno-honor-nans", "--cuda-device-only", "-S", SRC, "-o", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True)
+    return out.read_text()
+
+
+def _blocks(asm, name):
+    i = asm.index(name + ":")
+    j = asm.index(".Lfunc_end", i)
+    blocks, cur = [], []
+    for line in asm[i:j].split("\n"):
+        if re.match(r"^(\.LBB|; %bb\.)", line):
+            blocks.append(cur)
+            cur = [line]
+        else:
+            cur.append(line)
+    blocks.append(cur)
+    return blocks
+
+
+@pytest.mark.parametrize("name", KERNELS)
+def test_no_scratch_reload_in_dma_issue_blocks(fwd_asm, name):
+    bad = [b[0] for b in _blocks(fwd_asm, name)
+           if any("offen lds" in l for l in b) and any("scratch_load" in l for l in b)]
+    assert not bad, f"{name}: spill reloads in LDS-DMA issue blocks {bad[:4]}"

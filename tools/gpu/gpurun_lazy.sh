@@ -1,0 +1,8 @@
+#!/bin/bash
+# lazy-max forward: GPU suite (fail fast), slow-path frequency, A/B against the exact-max builds
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python tools/lazy_count.py lazycnt 2>&1 | grep -v amdgpu.ids
+timeout -k 10 400 python tools/ab.py ${AB:-base diagbase diag diagnochk base diag} 2>&1 | grep -v amdgpu.ids

@@ -26,9 +26,17 @@
 
 namespace vb {
 
+#ifndef VB_LAZY_COUNT
+#define VB_LAZY_COUNT 0   // diagnostic builds: count lazy-max slow paths (g_vb_stamp[10]) per tile half ([11])
+#endif
+#ifndef VB_LAZY_NOCHECK
+#define VB_LAZY_NOCHECK 0   // diagnostic builds only: no overflow check (timing of the fast path alone)
+#endif
+#if VB_DIAG || VB_LAZY_COUNT
+__device__ unsigned long long g_vb_stamp[16];
+#endif
 #if VB_DIAG
 // diagnostic-only cycle stamps (never in the product build): per-segment sums of s_memtime
-__device__ unsigned long long g_vb_stamp[16];
 __device__ __forceinline__ unsigned long long vb_stamp() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -53,6 +61,8 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   // no per-score v_fma before the v_exp (the D=64 loop is VALU-issue-bound). The extra rounding of
   // q*scale to 16 bits stays within the stated tolerance; launches that return the LSE for a
   // backward keep the unscaled Q so forward and backward see the same scores.
+  constexpr bool kLazy = kCBias && VB_FWD_LAZY && !VB_MFMA_ROWSUM && !VB_DIAG;
+  constexpr float kLazyBound = std::is_same<T, BF16>::value ? kLazyBoundBF16 : kLazyBoundF16;
   constexpr int kRowB = D * 2;                 // bytes per key row
   constexpr int kMatBytes = kKT * kRowB;       // one 64-key K (or V) tile
   constexpr int kBufBytes = 2 * kMatBytes;     // K image then V image
@@ -145,6 +155,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     }
   } else if (threadIdx.x < 64) {
     int n = 0;
+    int dpos = -1;   // list position of the diagonal block (key block qblk), if kept
     if (p.use_main) {
       for (int j0 = 0; j0 < nbk; j0 += 64) {
         const int j = j0 + lane;
@@ -154,8 +165,22 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
           const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
           list[pos] = (uint16_t)j;
+          if (j == qblk) dpos = pos;
         }
         n += __popcll(bal);
+      }
+      // Diagonal block first: in the Gilbert order a q-block's own key block usually holds its
+      // largest scores, so the running max is set once on the first tile (fewer rescales; the
+      // lazy-max launches rarely leave their fast path). Placement only: same sum, other order.
+      // The last key block keeps its place (a half-empty tail tile must stay the last tile).
+      const unsigned long long db = __ballot(dpos > 0);
+      if (db != 0 && qblk != nbk - 1) {
+        const int dp = __builtin_amdgcn_readlane(dpos, (int)__builtin_ctzll(db));
+        if (lane == 0) {
+          const uint16_t t = list[0];
+          list[0] = (uint16_t)qblk;
+          list[dp] = t;
+        }
       }
     }
     if (lane == 0) *list_n = n;
@@ -414,21 +439,6 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
         cur_bias = bias;
       }
     }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      typename T::vec8 kf[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(kl + kt * 32 * kRowB, k_lane[ks]);
-      if constexpr (kCBias) {
-        s[kt] = T::mfma32(kf[0], qf[0], cb);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
-        s[kt] = T::mfma32(kf[0], qf[0], s[kt]);
-      }
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) s[kt] = T::mfma32(kf[ks], qf[ks], s[kt]);
-    }
     // V^T fragments (ds_read_b64_tr_b16) for the first VPRE k-steps, issued before the softmax
     // VALU so they land while it runs; the rest are fetched one k-step ahead inside the PV loop.
     constexpr int VPRE = (D == 64 && !VB_MFMA_ROWSUM) ? VB_VPRE64 : 2;
@@ -446,6 +456,149 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       for (int dt = 0; dt < DT; ++dt)
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[kk][dt]), "+v"(vhi[kk][dt]));
     };
+    auto mask_tail = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= klen) s[kt][r] = -INFINITY;
+    };
+    // row max of one 32-key half (this lane's 16 values): 7 v_max3 + 1 v_max
+    auto half_max = [&](const f32x16& x) __attribute__((always_inline)) -> float {
+      const float a = max3f(max3f(max3f(x[0], x[1], x[2]), x[3], x[4]), x[5], x[6]);
+      const float c = max3f(max3f(max3f(x[8], x[9], x[10]), x[11], x[12]), x[13], x[14]);
+      return max3f(a, c, fmaxf(x[7], x[15]));
+    };
+    auto compute_s = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        typename T::vec8 kf[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(kl + kt * 32 * kRowB, k_lane[ks]);
+        if constexpr (kCBias) {
+          s[kt] = T::mfma32(kf[0], qf[0], cb);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
+          s[kt] = T::mfma32(kf[0], qf[0], s[kt]);
+        }
+#pragma unroll
+        for (int ks = 1; ks < KS; ++ks) s[kt] = T::mfma32(kf[ks], qf[ks], s[kt]);
+      }
+    };
+    // P = exp2(S) of one half packed to the storage type (the PV operands of k-steps 2kt, 2kt+1)
+    // WITHOUT overwriting S; returns the lane's fp32 sum (four independent chains)
+    auto exp_pack = [&](const f32x16& x, typename T::vec8& p0, typename T::vec8& p1) __attribute__((always_inline)) -> float {
+      float e[16];
+      float h4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        e[r] = exp2_fast(x[r]);
+        h4[r & 3] += e[r];
+      }
+      u32x4 u0, u1;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        u0[w] = pack2<T>(e[2 * w], e[2 * w + 1]);
+        u1[w] = pack2<T>(e[8 + 2 * w], e[8 + 2 * w + 1]);
+      }
+      p0 = __builtin_bit_cast(typename T::vec8, u0);
+      p1 = __builtin_bit_cast(typename T::vec8, u1);
+      return (h4[0] + h4[1]) + (h4[2] + h4[3]);
+    };
+    auto pv_pk = [&](int kk, const typename T::vec8& pf) __attribute__((always_inline)) {
+      wait_v(kk);
+      if (kk + VPRE < 4) read_v(kk + VPRE);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo[kk][dt], vhi[kk][dt]), pf, o[dt]);
+    };
+    // raise m by the rows' max mt of S (if > 0), rescaling O, l, the C seed and the S halves >= kt0
+    // (a half whose P is already in O is dead: touching it would keep it live)
+    auto raise_m = [&](float mt, auto KT0) __attribute__((always_inline)) {
+      constexpr int kt0 = decltype(KT0)::value;
+      const float delta = fmaxf(max_xor32(mt), 0.f);
+      const float alpha = exp2_fast(-delta);
+      m += delta;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < DT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        cb[r] -= delta;
+        if (kt0 == 0) s[0][r] -= delta;
+        s[1][r] -= delta;
+      }
+    };
+    if constexpr (kLazy) {
+      // Lazy running max (inference launches). The first tile takes its exact row max; after that
+      // no per-tile max is computed: P = exp2(S - m) uses the standing m, and the row sum of each
+      // half-tile (>= each of its P) is checked against kLazyBound. A passing check bounds every P,
+      // and so O and l, far from overflow. P is packed into separate registers, so S survives the
+      // exp: a failing check (rare, wave-uniform) raises m to the rows' max of that S, rescales O
+      // and l, and redoes the exp. m never exceeds the true running max, so l >= 1 after the first
+      // tile, and P's bf16 rounding is relative: the result equals the exact-max form up to
+      // rounding.
+      compute_s();
+#pragma unroll
+      for (int kk = 0; kk < VPRE; ++kk) read_v(kk);
+      if (klen < kKT) {
+        asm volatile("");
+        mask_tail(0);
+        mask_tail(1);
+      }
+      if (first) {
+        asm volatile("");
+        const float mt = max_xor32(fmaxf(half_max(s[0]), half_max(s[1])));
+        m += mt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s[0][r] -= mt;
+          s[1][r] -= mt;
+          cb[r] -= mt;
+        }
+        first = false;
+      }
+      typename T::vec8 pf[4];
+      if constexpr (kSplitPV) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          float hs = exp_pack(s[kt], pf[2 * kt], pf[2 * kt + 1]);
+          if (!VB_LAZY_NOCHECK && !__all(hs <= kLazyBound)) {
+            asm volatile("");
+#if VB_LAZY_COUNT
+            if (lane == 0) atomicAdd(&g_vb_stamp[10], 1ull);
+#endif
+            // O and l already hold the first half's P when kt = 1: they are rescaled with the rest
+            if (kt == 0) raise_m(half_max(s[0]), std::integral_constant<int, 0>{});
+            else raise_m(half_max(s[1]), std::integral_constant<int, 1>{});
+            hs = exp_pack(s[kt], pf[2 * kt], pf[2 * kt + 1]);
+          }
+          l += hs;
+          pv_pk(2 * kt, pf[2 * kt]);
+          pv_pk(2 * kt + 1, pf[2 * kt + 1]);
+        }
+      } else {
+        float h0 = exp_pack(s[0], pf[0], pf[1]);
+        float h1 = exp_pack(s[1], pf[2], pf[3]);
+        if (!VB_LAZY_NOCHECK && !__all(fmaxf(h0, h1) <= kLazyBound)) {
+          asm volatile("");
+#if VB_LAZY_COUNT
+          if (lane == 0) atomicAdd(&g_vb_stamp[10], 1ull);
+#endif
+          raise_m(fmaxf(half_max(s[0]), half_max(s[1])), std::integral_constant<int, 0>{});
+          h0 = exp_pack(s[0], pf[0], pf[1]);
+          h1 = exp_pack(s[1], pf[2], pf[3]);
+        }
+        l += h0 + h1;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) pv_pk(kk, pf[kk]);
+      }
+#if VB_LAZY_COUNT
+      if (lane == 0) atomicAdd(&g_vb_stamp[11], kSplitPV ? 2ull : 1ull);
+#endif
+      return;
+    }
+    compute_s();
 #pragma unroll
     for (int kk = 0; kk < VPRE; ++kk) read_v(kk);
     VB_STAMP(s1);
@@ -734,7 +887,7 @@ static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr
 
 }  // namespace vb
 
-#if VB_DIAG
+#if VB_DIAG || VB_LAZY_COUNT
 extern "C" int vb_diag_stamps(unsigned long long* host16, int reset) {
   (void)hipDeviceSynchronize();
   (void)hipMemcpyFromSymbol(host16, HIP_SYMBOL(vb::g_vb_stamp), sizeof(unsigned long long) * 16);

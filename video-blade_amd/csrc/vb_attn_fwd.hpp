@@ -29,7 +29,7 @@ struct FwdParams {
 #define VB_DIAG 0
 #endif
 #ifndef VB_VPRE64
-#define VB_VPRE64 4   // V^T k-steps prefetched before the softmax (D=64)
+#define VB_VPRE64 3   // V^T k-steps prefetched before the softmax (D=64); 4 spills the lazy-max loop
 #endif
 #ifndef VB_MFMA_ROWSUM
 #define VB_MFMA_ROWSUM 0
@@ -39,6 +39,9 @@ struct FwdParams {
 #endif
 #ifndef VB_FWD_CBIAS
 #define VB_FWD_CBIAS 1      // S accumulator seeded with (bias - m), Q pre-scaled: no per-score fma
+#endif
+#ifndef VB_FWD_LAZY
+#define VB_FWD_LAZY 1       // inference launches: no per-tile row max (checked row sums instead)
 #endif
 #ifndef VB_FWD_WAVES_D64
 #define VB_FWD_WAVES_D64 3  // waves per SIMD the D=64 kernel is register-budgeted for
@@ -52,6 +55,11 @@ constexpr int kMaxBlocks = 1024;  // keys <= 131072
 #define VB_RESCALE_SLACK 4.0f
 #endif
 constexpr float kRescaleSlack = VB_RESCALE_SLACK;  // log2 units: P <= 16 between rescales
+// lazy-max mode: a half-tile row sum (>= each of its P) above this raises m. bf16 P: with
+// P <= 2^32, O and l stay below 2^32 * Lk * max|V| (Lk <= 2^17): no overflow for any |V| < 2^78.
+// f16 P (max 65504): P <= 2^8, so P keeps the same normal range below it as P <= 1 does.
+constexpr float kLazyBoundBF16 = 4294967296.0f;
+constexpr float kLazyBoundF16 = 256.0f;
 
 // ---- LDS images --------------------------------------------------------------------------------
 // K: [64 rows][D] with 16-byte chunks XOR-swizzled so a ds_read_b128 column slice (32 rows, one
