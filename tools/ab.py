@@ -81,6 +81,11 @@ def main():
                 _lib._lib = libs[t]
                 out = fn()
                 torch.cuda.synchronize()
+                if a.what == "pred":   # the same scores and energy rule: masks must be identical
+                    if ref is None:
+                        ref = out[1].clone()
+                    else:
+                        print(f"  {t}: mask identical to {a.tags[0]}: {torch.equal(out[1], ref)}")
                 if a.what in ("attn", "bwd"):
                     if ref is None:
                         ref = out.float()

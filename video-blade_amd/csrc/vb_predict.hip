@@ -20,8 +20,11 @@
 
 namespace vb {
 
-constexpr int kPThreads = 256;
-constexpr int kPWaves = 4;
+#ifndef VB_PRED_WAVES
+#define VB_PRED_WAVES 4   // sampled q-blocks (one per wave) sharing one K stream through LDS
+#endif
+constexpr int kPWaves = VB_PRED_WAVES;
+constexpr int kPThreads = 64 * kPWaves;
 constexpr int kMaxNb = 320;        // sampled blocks per side (L <= 40960 at block 128)
 // keys per LDS tile: D=64 streams four 32-key sampled blocks per barrier (16 MFMAs per wave),
 // D=128 two (also 16 MFMAs); a 3-deep ring keeps the LDS at 48 KiB (3 workgroups per CU)
@@ -51,7 +54,7 @@ struct PredParams {
   void* po;
   uint8_t* mask;
   unsigned long long* count;
-  int dbg;   // diagnostic builds only (VB_DEBUG_PRED): 1 = skip epilogue, 2 = skip main loop
+  int dbg;   // diagnostic builds only (VB_DEBUG_PRED): 1 = skip epilogue, 2 = skip main loop, 4 = no MFMA
 };
 
 #ifndef VB_DIAG
@@ -218,6 +221,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   constexpr int kRowsPerInst = 1024 / kRowB;          // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerWave = kTileBytes / 1024 / kPWaves;
   constexpr int kBufs = kPBufs<D>;                    // tile t read, the younger ones in flight
+  constexpr int kSt = kKT / 2;                        // R stores per wave and tile
   // LDS: m [4][32] f32 | K tiles x4 (after the main loop: per-wave row scratch). The per-row
   // block maxima R go to a global scratch in [key block][32 rows] order (as the Triton kernel keeps
   // R in HBM): a tile's two columns are one contiguous 128-byte store, and the LDS stays small
@@ -288,19 +292,23 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
     k_lane[ks] = l32 * kRowB + 16 * ((2 * ks + half) ^ sw);
   }
   uint16_t* Rq = p.rbuf + ((int64_t)bh * nb + (wave_active ? qb : 0)) * nb * 32;   // this q-block
-  const srd_t rsrd = make_srd(Rq, nb * 64);
+  const srd_t rsrd = make_srd(Rq, wave_active ? nb * 64 : 0);
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
-    // retire this wave's DMA of tile t (younger tiles stay in flight), then the barrier makes
-    // every wave's part visible and guarantees tile t-1's buffer is no longer being read
-    const int younger = min(ntiles - 1 - t, kBufs - 2);
-    if (younger >= 2) VB_WAIT_VMCNT(2 * kInstPerWave);
-    else if (younger == 1) VB_WAIT_VMCNT(kInstPerWave);
-    else VB_WAIT_VMCNT(0);
+    // retire this wave's DMA of tile t, then the barrier makes every wave's part visible and
+    // guarantees tile t-1's buffer is no longer being read. vmcnt counts the R stores too, in issue
+    // order: younger than DMA(t) are the stores of the (up to kBufs-1) bodies since it was issued
+    // and the DMAs of tiles t+1 .. t+kBufs-2. Every body issues exactly kSt stores (see below), so
+    // the count is exact and the younger tiles' DMAs stay in flight.
+    const int nst = min(t, kBufs - 1);
+    const int ndma = max(0, min(kBufs - 2, ntiles - 1 - t));
+    if (nst == kBufs - 1 && ndma == kBufs - 2) VB_WAIT_VMCNT((kBufs - 1) * kSt + (kBufs - 2) * kInstPerWave);
+    else wait_vmcnt_upto<kBufs * kSt + kBufs * kInstPerWave>(nst * kSt + ndma * kInstPerWave);
     __builtin_amdgcn_s_barrier();
     if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
     const uint8_t* kl = ktile + u * kTileBytes;
+    if (VB_DIAG && (p.dbg & 4)) return;   // diagnostic: stream the K tiles only
     // one accumulator per 32-key block: the MFMAs of block kt+1 do not wait for the row-max
     // reads of block kt (a shared accumulator serialises MFMA -> s_nop -> VALU -> MFMA)
     f32x16 sc[kKT];
@@ -341,12 +349,12 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
     }
 #pragma unroll
     for (int pr = 0; pr < kKT / 2; ++pr) m = fmaxf(m, mxp[pr]);   // this half's blocks; halves meet below
-    // R[j][row]: lane (half, row) stores block j0 + 2pr + half, so one store writes 128 contiguous bytes
-    if (wave_active) {
+    // R[j][row]: lane (half, row) stores block j0 + 2pr + half, so one store writes 128 contiguous
+    // bytes. Issued unconditionally (kSt per body, the vmcnt arithmetic above relies on it): blocks
+    // past nb fall outside the descriptor and an inactive wave's descriptor is empty, so the
+    // hardware drops those lanes.
 #pragma unroll
-      for (int pr = 0; pr < kKT / 2; ++pr)
-        if (j0 + 2 * pr + half < nb) store16(rsrd, (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
-    }
+    for (int pr = 0; pr < kSt; ++pr) store16(rsrd, (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
     body(t0, std::integral_constant<int, 0>{});

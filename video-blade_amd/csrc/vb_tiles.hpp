@@ -17,6 +17,21 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 // s_waitcnt vmcnt(n) with lgkm/exp counters left at max (gfx9 encoding)
 #define VB_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, kMax] (the count is an instruction
+// immediate): a compile-time chain of scalar compares
+template <int kMax>
+__device__ __forceinline__ void wait_vmcnt_upto(int n) {
+  if constexpr (kMax > 0) {
+    if (n >= kMax) {
+      VB_WAIT_VMCNT(kMax);
+      return;
+    }
+    wait_vmcnt_upto<kMax - 1>(n);
+  } else {
+    VB_WAIT_VMCNT(0);
+  }
+}
+
 template <class T>
 __device__ __forceinline__ typename T::vec8 lds_b128(const uint8_t* base, int off) {
   return *reinterpret_cast<const typename T::vec8*>(base + off);
