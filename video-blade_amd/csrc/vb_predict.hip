@@ -35,6 +35,9 @@ template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
 #ifndef VB_PRED_SPLIT_ENERGY
 #define VB_PRED_SPLIT_ENERGY 0   // 1: the energy rule runs as its own kernel after the scores
 #endif
+#ifndef VB_PRED_SCHED
+#define VB_PRED_SCHED 4   // K-fragment reads issued this many MFMAs ahead (0: the compiler's order)
+#endif
 #ifndef VB_PRED_MIN_WG
 #define VB_PRED_MIN_WG 2
 #endif
@@ -323,6 +326,17 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) sc[kt] = T::mfma32(kf[ks], qf[ks], sc[kt]);
     }
+#if VB_PRED_SCHED
+    // Pin the issue order: each K-fragment read VB_PRED_SCHED MFMAs ahead of the MFMA that consumes
+    // it (left alone, hipcc reuses one fragment register and serialises read -> wait -> MFMA).
+#pragma unroll
+    for (int i = 0; i < VB_PRED_SCHED; ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+    for (int i = 0; i < kKT * KS; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      if (i + VB_PRED_SCHED < kKT * KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+#endif
     // row maxima, two 32-key blocks per v_permlane32_swap: after the swap lanes 0-31 hold block
     // 2pr's full row max and lanes 32-63 block 2pr+1's (the halves of each block's C tile meet)
     const int j0 = kKT * t;
