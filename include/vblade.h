@@ -116,8 +116,8 @@ typedef struct vb_predict_args {
   const void* q; const void* k;
   int64_t q_stride[3]; int64_t k_stride[3];
   const int32_t* rows;     /* [L] reordered -> caller row, or NULL */
-  const int32_t* q_off;    /* [B,H,num_keep] int32 in [0,block) */
-  const int32_t* k_off;
+  int32_t* q_off;          /* [B,H,num_keep] int32 in [0,block): input, or output with rand_q/rand_k */
+  int32_t* k_off;
   int B, H, L, D, block, num_keep;
   float scale;             /* <= 0 -> D^-1/2 */
   float energy_threshold;
@@ -132,6 +132,20 @@ typedef struct vb_predict_args {
   void* staged_event;      /* nullable hipEvent_t, recorded on `stream` once the sampled rows are
                               staged (before the score kernel): independent work on another stream
                               can start then and overlap the score kernel */
+  /* Optional fusions (NULL = off):
+   * rand_q/rand_k: [B,H,block] fp32 uniforms, the q then k torch.rand draws of
+   *   random_sample_tokens (:45-46); the topk(num_keep) offsets are drawn in the sampling launch
+   *   (as vb_sample_offsets) and WRITTEN to q_off/k_off.
+   * pool_*: the pooled K/V pass of vb_pool_kv (on this call's k and pool_v, same rows) run by
+   *   extra workgroups of the score kernel's own launch, beside it on `stream`: no second stream
+   *   and no events. pool_kp/pool_vp [B,H,ceil(L/pool_gap),D]; pool_k_r/pool_v_r [B,H,L,D] or NULL. */
+  const float* rand_q;
+  const float* rand_k;
+  const void* pool_v;
+  int64_t pool_v_stride[3];
+  int pool_gap;
+  void* pool_kp; void* pool_vp;
+  void* pool_k_r; void* pool_v_r;
 } vb_predict_args;
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);

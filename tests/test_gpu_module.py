@@ -118,3 +118,41 @@ def test_sparsity_statistic_is_device_side_and_matches_mask():
             m(q.to(DEV), k.to(DEV), v.to(DEV))
         vals.append(1 - m.last_mask.float().mean().item() - 1 / 15)
     assert abs(m.sparsity - sum(vals) / 3) < 1e-9
+
+
+@pytest.mark.parametrize("variant,D", [("cog", 64), ("wan", 128)])
+def test_fused_sampling_and_pool_launches_match_separate_launches(variant, D):
+    """The module's launch structure (topk offsets drawn inside the sampling launch, the pooled
+    K/V pass run by extra workgroups of the score kernel's launch) gives the same offsets, mask,
+    pooled K/V, Gilbert copies and output, bit for bit, as the separate launches (vb_sample_offsets,
+    vb_mask_predict with given offsets, vb_pool_kv) on the same RNG draws."""
+    import vblade
+    from vblade import ops
+    kw = dict(width=12, height=8, depth=6, text_length=26) if variant == "cog" else dict(width=13, height=6, depth=7)
+    fused = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **kw)
+    sep = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, overlap=False, **kw)
+    L = fused.gilbert_rearranger.seq_len
+    H = 3
+    g = torch.Generator(device=DEV).manual_seed(11)
+    q, k, v = (torch.randn(1, H, L, D, generator=g, device=DEV).bfloat16() for _ in range(3))
+    with torch.no_grad():
+        torch.manual_seed(5)
+        out_f = fused(q, k, v)
+        torch.manual_seed(5)
+        rq = torch.rand(1, H, 1, 128, device=DEV)
+        rk = torch.rand(1, H, 1, 128, device=DEV)
+        qo, ko = ops.sample_offsets(rq, rk, 32)
+        out_s = sep(q, k, v, q_off=qo[:, :, 0], k_off=ko[:, :, 0])
+        rows = fused._rows(q.device)
+        outs = ops.pool_kv_outputs(k, fused.sample_gap, reordered=True)
+        _, mask_p = ops.mask_predict(q, k, rows=rows, energy_threshold=0.95, min_keep=1, max_keep=4,
+                                     rand=(rq, rk), pool=(v, fused.sample_gap, outs))
+        _, mask_r = ops.mask_predict(q, k, qo[:, :, 0], ko[:, :, 0], rows=rows, energy_threshold=0.95,
+                                     min_keep=1, max_keep=4)
+        ref_pool = ops.pool_kv(k, v, fused.sample_gap, rows, reordered=True)
+    torch.cuda.synchronize()
+    assert torch.equal(fused.last_mask, sep.last_mask)
+    assert torch.equal(out_f, out_s)
+    assert torch.equal(mask_p, mask_r)
+    for a, b in zip(outs, ref_pool):
+        assert torch.equal(a, b)

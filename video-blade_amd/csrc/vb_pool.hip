@@ -4,61 +4,14 @@
 //   + the rearrange gathers (:148-150); the bf16 combine of adaptive_block_sparse_attn (:374-393).
 #include <cstdlib>
 
-#include "vb_common.hpp"
+#include "vb_pool.hpp"
 
 namespace vb {
 
-// simple_pooling of K and V: one thread per 16-byte chunk of a pooled row. Every reordered row
-// is read by exactly one thread, which (when k_r/v_r are given) also writes it to the contiguous
-// Gilbert-ordered copies the attention kernel streams (the reference's index_select, fused).
+// simple_pooling of K and V (+ the Gilbert-ordered copies): pool_kv_span (vb_pool.hpp), grid-strided
 template <class T>
-__global__ void __launch_bounds__(256) pool_kv_kernel(const uint8_t* k, const uint8_t* v, int64_t ks0, int64_t ks1,
-                                                      int64_t ks2, int64_t vs0, int64_t vs1, int64_t vs2,
-                                                      const int32_t* rows, int B, int H, int L, int D, int gap,
-                                                      int Lp, uint8_t* kp, uint8_t* vp, uint8_t* k_r,
-                                                      uint8_t* v_r) {
-  const int CH = D / 8;
-  const int64_t total = (int64_t)B * H * Lp * CH;
-  // grid-stride: the launch may use fewer workgroups than chunks (see pool_grid below)
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-  const int ch = idx % CH;
-  const int64_t prow = idx / CH;        // (b*H + h)*Lp + pr
-  const int pr = prow % Lp;
-  const int bh = prow / Lp;
-  const int b = bh / H, h = bh % H;
-  float ak[8], av[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ak[e] = av[e] = 0.f;
-  for (int t = 0; t < gap; ++t) {
-    const int g = pr * gap + t;
-    int pos = min(g, L - 1);  // replicate padding
-    if (rows) pos = rows[pos];
-    const u32x4 xk = *reinterpret_cast<const u32x4*>(k + 2 * (b * ks0 + h * ks1 + (int64_t)pos * ks2) + ch * 16);
-    const u32x4 xv = *reinterpret_cast<const u32x4*>(v + 2 * (b * vs0 + h * vs1 + (int64_t)pos * vs2) + ch * 16);
-    if (k_r && g < L) {
-      const int64_t o = ((int64_t)bh * L + g) * D * 2 + ch * 16;
-      *reinterpret_cast<u32x4*>(k_r + o) = xk;
-      *reinterpret_cast<u32x4*>(v_r + o) = xv;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      ak[2 * e] += T::bits_to_f32(xk[e] & 0xffff);
-      ak[2 * e + 1] += T::bits_to_f32(xk[e] >> 16);
-      av[2 * e] += T::bits_to_f32(xv[e] & 0xffff);
-      av[2 * e + 1] += T::bits_to_f32(xv[e] >> 16);
-    }
-  }
-  const float f = 1.0f / (float)gap;  // mean = sum * (1/N), as ATen's MeanOps
-  u32x4 ok, ov;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    ok[e] = pack2<T>(ak[2 * e] * f, ak[2 * e + 1] * f);
-    ov[e] = pack2<T>(av[2 * e] * f, av[2 * e + 1] * f);
-  }
-  *reinterpret_cast<u32x4*>(kp + (prow * D + ch * 8) * 2) = ok;
-  *reinterpret_cast<u32x4*>(vp + (prow * D + ch * 8) * 2) = ov;
-  }
+__global__ void __launch_bounds__(256) pool_kv_kernel(const PoolTask t) {
+  pool_kv_span<T>(t, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 // Workgroups of an HBM-bound pass that runs beside the predictor's score kernel on another stream:
@@ -121,22 +74,18 @@ extern "C" int vb_pool_kv(const void* k, const void* v, const int64_t* k_stride,
   if (B <= 0 || H <= 0 || L <= 0 || gap <= 0 || D % 8) return fail(VB_ERR_INVALID, "vb_pool_kv: bad sizes");
   for (int i = 0; i < 3; ++i)
     if ((k_stride[i] | v_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_pool_kv: strides must be multiples of 8");
-  const int Lp = (L + gap - 1) / gap;
-  const int64_t total = (int64_t)B * H * Lp * (D / 8);
-  const dim3 grid(pool_grid(total));
+  PoolTask t{};
+  t.k = reinterpret_cast<const uint8_t*>(k); t.v = reinterpret_cast<const uint8_t*>(v);
+  for (int i = 0; i < 3; ++i) { t.ks[i] = k_stride[i]; t.vs[i] = v_stride[i]; }
+  t.rows = rows; t.B = B; t.H = H; t.L = L; t.D = D; t.gap = gap; t.Lp = (L + gap - 1) / gap;
+  t.kp = reinterpret_cast<uint8_t*>(kp); t.vp = reinterpret_cast<uint8_t*>(vp);
+  t.k_r = reinterpret_cast<uint8_t*>(k_r); t.v_r = reinterpret_cast<uint8_t*>(v_r);
+  const dim3 grid(pool_grid((int64_t)B * H * t.Lp * (D / 8)));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  auto* kb = reinterpret_cast<const uint8_t*>(k);
-  auto* vb_ = reinterpret_cast<const uint8_t*>(v);
   if (dtype == VB_DTYPE_BF16)
-    hipLaunchKernelGGL(pool_kv_kernel<BF16>, grid, dim3(256), 0, s, kb, vb_, k_stride[0], k_stride[1], k_stride[2],
-                       v_stride[0], v_stride[1], v_stride[2], rows, B, H, L, D, gap, Lp,
-                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp),
-                       reinterpret_cast<uint8_t*>(k_r), reinterpret_cast<uint8_t*>(v_r));
+    hipLaunchKernelGGL(pool_kv_kernel<BF16>, grid, dim3(256), 0, s, t);
   else if (dtype == VB_DTYPE_F16)
-    hipLaunchKernelGGL(pool_kv_kernel<F16>, grid, dim3(256), 0, s, kb, vb_, k_stride[0], k_stride[1], k_stride[2],
-                       v_stride[0], v_stride[1], v_stride[2], rows, B, H, L, D, gap, Lp,
-                       reinterpret_cast<uint8_t*>(kp), reinterpret_cast<uint8_t*>(vp),
-                       reinterpret_cast<uint8_t*>(k_r), reinterpret_cast<uint8_t*>(v_r));
+    hipLaunchKernelGGL(pool_kv_kernel<F16>, grid, dim3(256), 0, s, t);
   else
     return fail(VB_ERR_INVALID, "vb_pool_kv: unknown dtype");
   return check_launch("pool_kv_kernel");

@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "vb_tiles.hpp"
+#include "vb_pool.hpp"
 
 namespace vb {
 
@@ -42,6 +43,10 @@ template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
 #define VB_PRED_MIN_WG 2
 #endif
 template <int D> constexpr int kPBufs = VB_PRED_BUFS;
+#ifndef VB_FUSED_POOL_WGS
+#define VB_FUSED_POOL_WGS 256   // workgroups of the predictor's launch that run the pooled K/V pass
+#endif
+constexpr int kFusedPoolWgs = VB_FUSED_POOL_WGS;
 
 struct PredParams {
   const void* q; const void* k;
@@ -49,7 +54,10 @@ struct PredParams {
   uint8_t* q_s; uint8_t* k_s;   // sampled k rows [B,H,nb*32,D] contiguous (workspace); q_s unused
   uint16_t* rbuf;               // R [B,H,nb(q-block),nb(key block),32 rows] storage bits (workspace)
   const int32_t* rows;
-  const int32_t* q_off; const int32_t* k_off;
+  int32_t* q_off; int32_t* k_off;   // inputs, or outputs when rand_q/rand_k are given
+  const float* rand_q; const float* rand_k;   // [B,H,block] uniforms (nullable): offsets drawn here
+  PoolTask pool;                    // pooled K/V pass run by the first n_pool workgroups (fused launch)
+  int n_pool;
   int B, H, L, D, block, nb;
   float c;             // fp32(scale) * fp32(1.44269504), as the Triton kernel forms qk_scale
   float thr;
@@ -178,29 +186,57 @@ __device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int n
   }
 }
 
+// random_sample_tokens' topk (cogvideo_blocksparseattn.py:45-46) by one wave: the indices of the
+// `keep` largest of n <= 256 uniforms r (global), in descending order of value, ties -> lower index
+// first, written to dst[rank] (LDS or global). `sv` is LDS scratch for n floats.
+__device__ __forceinline__ void topk_wave(const float* r, int n, int keep, int32_t* dst, float* sv) {
+  const int lane = threadIdx.x & 63;
+  for (int i = lane; i < n; i += 64) sv[i] = r[i];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const float v = i < n ? sv[i] : 0.f;
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+      const float w = sv[j];   // LDS broadcast
+      rank += (w > v || (w == v && j < i)) ? 1 : 0;
+    }
+    if (i < n && rank < keep) dst[rank] = i;
+  }
+}
+
 // Sampled rows of k, gathered once into contiguous [B,H,nb*32,D] (the q fragments are gathered by the
 // predictor's prologue directly, one row per lane):
 // row j*32 + t of (b,h) = reordered position min(j*block + off[b,h,t], L-1) (replicate padding),
 // read at the caller's row rows[pos]. The predictor then streams K by plain LDS-DMA.
+// grid (row chunks, B*H). With rand_q/rand_k the offsets are drawn here first (topk_wave: one launch
+// instead of two) and the first chunk of every (b,h) writes them out for the score kernel.
 template <class T>
 __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
+  __shared__ float sv[2][256];
+  __shared__ int32_t koff_s[32];
+  const int bh = blockIdx.y;
+  const int wave = threadIdx.x >> 6;
+  const int32_t* koff = p.k_off + (int64_t)bh * 32;
+  if (p.rand_k) {
+    if (wave == 0) topk_wave(p.rand_k + (int64_t)bh * p.block, p.block, 32, koff_s, sv[0]);
+    if (blockIdx.x == 0 && wave == 1)
+      topk_wave(p.rand_q + (int64_t)bh * p.block, p.block, 32, p.q_off + (int64_t)bh * 32, sv[1]);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < 32) p.k_off[(int64_t)bh * 32 + threadIdx.x] = koff_s[threadIdx.x];
+    koff = koff_s;
+  }
   // one thread per sampled row: the two index loads once, then D/8 independent 16-byte copies
-  const int CH = p.D / 8;
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nrow = (int64_t)p.nb * 32;
-  if (r >= (int64_t)p.B * p.H * nrow) return;
-  const bool isk = true;   // q rows are gathered by the predictor itself
-  const int jt = r % nrow;
-  const int bh = r / nrow;
+  const int jt = blockIdx.x * blockDim.x + threadIdx.x;
+  if (jt >= p.nb * 32) return;
   const int b = bh / p.H, h = bh % p.H;
-  const int32_t* off = (isk ? p.k_off : p.q_off) + (int64_t)bh * 32;
-  int pos = min((jt >> 5) * p.block + off[jt & 31], p.L - 1);
+  int pos = min((jt >> 5) * p.block + koff[jt & 31], p.L - 1);
   if (p.rows) pos = p.rows[pos];
-  const int64_t* st = isk ? p.ks : p.qs;
-  const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(isk ? p.k : p.q) +
-                                                    2 * (b * st[0] + h * st[1] + (int64_t)pos * st[2]));
-  u32x4* dst = reinterpret_cast<u32x4*>(p.k_s + r * p.D * 2);
-  if (CH == 8) {
+  const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(p.k) +
+                                                    2 * (b * p.ks[0] + h * p.ks[1] + (int64_t)pos * p.ks[2]));
+  u32x4* dst = reinterpret_cast<u32x4*>(p.k_s + ((int64_t)bh * p.nb * 32 + jt) * p.D * 2);
+  if (p.D == 64) {
     u32x4 x[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) x[c] = src[c];
@@ -229,6 +265,14 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // block maxima R go to a global scratch in [key block][32 rows] order (as the Triton kernel keeps
   // R in HBM): a tile's two columns are one contiguous 128-byte store, and the LDS stays small
   // enough for 3 workgroups per CU at any nb.
+  // The first n_pool workgroups of the launch run the pooled K/V pass (HBM-bound) beside the score
+  // workgroups (MFMA-bound): one launch, no second stream or events. n_pool is a multiple of 8, so
+  // the score workgroups keep their XCD (blockIdx % 8).
+  if ((int)blockIdx.x < p.n_pool) {
+    pool_kv_span<T>(p.pool, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)p.n_pool * blockDim.x);
+    return;
+  }
+  const int wg = (int)blockIdx.x - p.n_pool;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nb = p.nb;
   float* mrow_s = reinterpret_cast<float*>(smem);
@@ -242,7 +286,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // XCD-aware order: give each XCD a contiguous range of (head, q-group) work, so a head's sampled
   // keys are re-read from that XCD's own L2. Placement only affects speed.
   const int nqg = (nb + kPWaves - 1) / kPWaves;
-  const int lin = xcd_linear(blockIdx.x, nqg * p.B * p.H);
+  const int lin = xcd_linear(wg, nqg * p.B * p.H);
   const int bh = lin / nqg;
   const int qb = (lin % nqg) * kPWaves + wave;  // this wave's sampled q-block
   const bool wave_active = qb < nb;
@@ -440,25 +484,10 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
 __global__ void __launch_bounds__(256) topk_offsets_kernel(const float* rq, const float* rk, int rows, int n,
                                                            int keep, int32_t* oq, int32_t* ok) {
   __shared__ float buf[4][256];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows || n > 256) return;
-  const float* r = (blockIdx.y ? rk : rq) + (int64_t)row * n;
-  int32_t* o = (blockIdx.y ? ok : oq) + (int64_t)row * keep;
-  float* sv = buf[wave];
-  for (int i = lane; i < n; i += 64) sv[i] = r[i];
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  for (int i0 = 0; i0 < n; i0 += 64) {
-    const int i = i0 + lane;
-    const float v = i < n ? sv[i] : 0.f;
-    int rank = 0;
-    for (int j = 0; j < n; ++j) {
-      const float w = sv[j];   // LDS broadcast
-      rank += (w > v || (w == v && j < i)) ? 1 : 0;
-    }
-    if (i < n && rank < keep) o[rank] = i;
-  }
+  topk_wave((blockIdx.y ? rk : rq) + (int64_t)row * n, n, keep, (blockIdx.y ? ok : oq) + (int64_t)row * keep, buf[wave]);
 }
 
 template <class T>
@@ -506,11 +535,11 @@ static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t st
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)smem) != hipSuccess)
     return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
-  const int64_t gthreads = (int64_t)p.B * p.H * p.nb * 32;
-  hipLaunchKernelGGL(sample_rows_kernel<T>, dim3((unsigned)((gthreads + 255) / 256), 1), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(sample_rows_kernel<T>, dim3((unsigned)((p.nb * 32 + 255) / 256), (unsigned)(p.B * p.H)), dim3(256),
+                     0, stream, p);
   if (int rc = check_launch("sample_rows_kernel")) return rc;
   if (staged && hipEventRecord(staged, stream) != hipSuccess) return fail(VB_ERR_LAUNCH, "vb_mask_predict: hipEventRecord failed");
-  const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H);
+  const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H + p.n_pool);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
   if (int rc = check_launch("mask_predict_kernel")) return rc;
   if (VB_PRED_SPLIT_ENERGY && p.mask) {
@@ -561,6 +590,26 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   p.q_s = nullptr;
   p.k_s = reinterpret_cast<uint8_t*>(a->workspace);
   p.rbuf = reinterpret_cast<uint16_t*>(p.k_s + rows_b);
+  if ((a->rand_q == nullptr) != (a->rand_k == nullptr))
+    return fail(VB_ERR_INVALID, "vb_mask_predict: give both rand_q and rand_k or neither");
+  p.rand_q = a->rand_q; p.rand_k = a->rand_k;
+  if (a->pool_kp) {   // the pooled K/V pass rides in the score kernel's launch
+    if (!a->pool_v || !a->pool_vp || a->pool_gap <= 0 || ((a->pool_k_r == nullptr) != (a->pool_v_r == nullptr)))
+      return fail(VB_ERR_INVALID, "vb_mask_predict: pool_v, pool_vp, pool_gap > 0 and both or neither of pool_k_r/pool_v_r");
+    for (int i = 0; i < 3; ++i)
+      if (a->pool_v_stride[i] & 7) return fail(VB_ERR_INVALID, "vb_mask_predict: pool_v strides must be multiples of 8");
+    PoolTask& t = p.pool;
+    t.k = reinterpret_cast<const uint8_t*>(a->k); t.v = reinterpret_cast<const uint8_t*>(a->pool_v);
+    for (int i = 0; i < 3; ++i) { t.ks[i] = a->k_stride[i]; t.vs[i] = a->pool_v_stride[i]; }
+    t.rows = a->rows; t.B = a->B; t.H = a->H; t.L = a->L; t.D = a->D; t.gap = a->pool_gap;
+    t.Lp = (a->L + a->pool_gap - 1) / a->pool_gap;
+    t.kp = reinterpret_cast<uint8_t*>(a->pool_kp); t.vp = reinterpret_cast<uint8_t*>(a->pool_vp);
+    t.k_r = reinterpret_cast<uint8_t*>(a->pool_k_r); t.v_r = reinterpret_cast<uint8_t*>(a->pool_v_r);
+    const int64_t items = (int64_t)a->B * a->H * t.Lp * (a->D / 8);
+    int n = (int)((items + 255) / 256);
+    n = n < kFusedPoolWgs ? n : kFusedPoolWgs;
+    p.n_pool = (n + 7) / 8 * 8;   // keeps blockIdx % 8 of the score workgroups (their XCD)
+  }
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);
 #endif

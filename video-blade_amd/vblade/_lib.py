@@ -54,6 +54,9 @@ class PredictArgs(ctypes.Structure):
         ("dtype", ctypes.c_int),
         ("workspace", _vp), ("workspace_bytes", ctypes.c_uint64),
         ("staged_event", _vp),
+        ("rand_q", _vp), ("rand_k", _vp),
+        ("pool_v", _vp), ("pool_v_stride", _i64x3), ("pool_gap", ctypes.c_int),
+        ("pool_kp", _vp), ("pool_vp", _vp), ("pool_k_r", _vp), ("pool_v_r", _vp),
     ]
 
 

@@ -187,12 +187,16 @@ class AdaptiveBlockSparseAttn(nn.Module):
         return getattr(self, "_folded", 0.0) / self.sparsity_counter
 
     # -------------------------------------------------------------------------------- forward
-    def predict_mask(self, q, k, q_off=None, k_off=None, count=None, staged_event=None):
-        """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores."""
+    def predict_mask(self, q, k, q_off=None, k_off=None, count=None, staged_event=None, pool=None):
+        """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores. ``pool``
+        (v, gap, outs) runs the pooled K/V pass inside the score kernel's launch."""
         B, H, L, D = q.shape
+        rand = None
         if q_off is None and k_off is None:
-            q_off, k_off = draw_sample_offsets_qk(B, H, q.device, self.block, self.num_keep)
-        if q_off is None:
+            # the reference's two draws (:77-78, q first); topk runs inside the sampling launch
+            rand = (torch.rand(B, H, 1, self.block, device=q.device),
+                    torch.rand(B, H, 1, self.block, device=q.device))
+        elif q_off is None:
             q_off = draw_sample_offsets(B, H, q.device)
         if k_off is None:
             k_off = draw_sample_offsets(B, H, q.device)
@@ -201,7 +205,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
         po, mask = ops.mask_predict(q, k, q_off, k_off, rows=self._rows(q.device),
                                     energy_threshold=self.energy_threshold, min_keep=lo,
                                     max_keep=hi, force_tail=self.force_tail, mask_count=count,
-                                    staged_event=staged_event)
+                                    staged_event=staged_event, rand=rand, pool=pool)
         return po, mask
 
     def forward(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *,
@@ -215,24 +219,22 @@ class AdaptiveBlockSparseAttn(nn.Module):
         nb = (L + self.block - 1) // self.block
         count = self._count_slot(q.device)
         grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)
-        # inference: the pooled K/V pass (HBM-bound) runs on a side stream beside the mask
-        # predictor (MFMA-bound); they are independent within the call
         fused = not grad and self.combine != "reference"
         pooled = None
         if block_mask is None:
             # inference: the pooled K/V pass (one pass over K/V: pooled K/V + the Gilbert-ordered
-            # contiguous copies the attention kernel streams by LDS-DMA; HBM-bound) runs on a side
-            # stream as soon as the predictor has staged its sampled rows, beside the MFMA-bound
-            # score kernel
-            ev = self._side.event(q.device) if (fused and self.overlap) else None
-            # the side stream's outputs are allocated first: the predictor's temporaries, freed
-            # while its score kernel still runs, must not be recycled into them
-            outs = ops.pool_kv_outputs(k, self.sample_gap, reordered=True) if fused else None
+            # contiguous copies the attention kernel streams by LDS-DMA; HBM-bound) runs inside the
+            # predictor's score-kernel launch, beside the MFMA-bound score workgroups (overlap=True),
+            # or after it (overlap=False)
+            ride = fused and self.overlap
+            outs = ops.pool_kv_outputs(k, self.sample_gap, reordered=True) if ride else None
             with torch.no_grad():
-                _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count, staged_event=ev)
-            if fused:
-                side = self._side.fork(q.device, event=ev) if self.overlap else None
-                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True, stream=side, out=outs)
+                _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count,
+                                            pool=(v, self.sample_gap, outs) if ride else None)
+            if ride:
+                pooled = outs
+            elif fused:
+                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True)
         else:
             mask = block_mask.to(torch.uint8)
             count.add_(mask.sum())
@@ -247,8 +249,6 @@ class AdaptiveBlockSparseAttn(nn.Module):
         else:
             # q rows gathered and out rows scattered inside the attention kernel
             kp, vp, k_r, v_r = pooled
-            if self.overlap and block_mask is None:
-                self._side.join(q.device)
             ev = self.attn_events
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)

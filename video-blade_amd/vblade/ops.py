@@ -281,19 +281,29 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
 # ----------------------------------------------------------------------------------------------
 # mask predictor, energy rule, pooling, combine
 # ----------------------------------------------------------------------------------------------
-def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_keep=1,
+def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.95, min_keep=1,
                  max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True,
-                 staged_event=None):
+                 staged_event=None, rand=None, pool=None):
     """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
     po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb] (None with want_mask=False: the scores
     only, no energy rule). ``staged_event`` (a torch.cuda.Event) is recorded once the sampled
-    rows are staged, before the score kernel: work waiting on it overlaps the score kernel."""
+    rows are staged, before the score kernel: work waiting on it overlaps the score kernel.
+
+    ``rand=(rand_q, rand_k)``: the fp32 uniforms [B,H,1,block] of random_sample_tokens instead of
+    q_off/k_off; the topk offsets are drawn inside the sampling launch.
+    ``pool=(v, gap, outs)``: the pooled K/V pass (vb_pool_kv of k, v through ``rows``) run by extra
+    workgroups of the score kernel's launch on the current stream; ``outs`` = pool_kv_outputs(k,
+    gap, reordered) receives kp, vp[, k_r, v_r]."""
     dev = _require_gpu(q, k, q_off, k_off, rows)
     q, k = _aligned_bhld(q), _aligned_bhld(k)
     B, H, L, D = q.shape
     nb = (L + BLOCK - 1) // BLOCK
     po = torch.empty(B, H, nb, nb, device=dev, dtype=q.dtype)
     mask = torch.empty(B, H, nb, nb, device=dev, dtype=torch.uint8) if want_mask else None
+    if rand is not None:
+        rand_q, rand_k = (r.float().contiguous() for r in rand)
+        q_off = torch.empty(B, H, 32, device=dev, dtype=torch.int32)
+        k_off = torch.empty(B, H, 32, device=dev, dtype=torch.int32)
     q_off = q_off.to(torch.int32).contiguous()
     k_off = k_off.to(torch.int32).contiguous()
     a = PredictArgs()
@@ -311,6 +321,19 @@ def mask_predict(q, k, q_off, k_off, *, rows=None, energy_threshold=0.95, min_ke
     ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
     a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
     a.staged_event = staged_event.cuda_event if staged_event is not None else None
+    if rand is not None:
+        if rand_q.shape[-1] != BLOCK or rand_q.numel() != B * H * BLOCK or rand_k.numel() != B * H * BLOCK:
+            raise ValueError("mask_predict: rand draws must be [B,H,1,block]")
+        a.rand_q, a.rand_k = rand_q.data_ptr(), rand_k.data_ptr()
+    if pool is not None:
+        v, gap, outs = pool
+        v = _aligned_bhld(v)
+        if v.shape != k.shape or outs[0].shape != (B, H, (L + int(gap) - 1) // int(gap), D):
+            raise ValueError("mask_predict: pool v must match k and outs come from pool_kv_outputs")
+        a.pool_v, a.pool_v_stride, a.pool_gap = v.data_ptr(), _s3(v), int(gap)
+        a.pool_kp, a.pool_vp = outs[0].data_ptr(), outs[1].data_ptr()
+        if len(outs) > 2:
+            a.pool_k_r, a.pool_v_r = outs[2].data_ptr(), outs[3].data_ptr()
     check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
 
