@@ -380,7 +380,7 @@ def cpu_baseline(variant, calls, frames):
     import bsa_oracle as O
     cfg = O.AdaptiveConfig.cogvideox() if variant == "cog" else O.AdaptiveConfig.wan()
     V = VARIANTS[variant]
-    heads = 2
+    heads = 24 if variant == "cog" else 6   # about 10 s of CPU work (half of one call's heads)
     L = cfg.width * cfg.height * cfg.depth + cfg.text_length
     g = torch.Generator().manual_seed(0)
     cent = torch.randn(1, heads, L // 128 + 1, V["D"], generator=g).repeat_interleave(128, 2)[:, :, :L]

@@ -198,7 +198,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
                     torch.rand(B, H, 1, self.block, device=q.device))
         elif q_off is None:
             q_off = draw_sample_offsets(B, H, q.device)
-        if k_off is None:
+        elif k_off is None:
             k_off = draw_sample_offsets(B, H, q.device)
         nb = (L + self.block - 1) // self.block
         lo, hi = retain_counts(nb, self.min_retain_ratio, self.max_retain_ratio, self.variant)
