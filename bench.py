@@ -374,7 +374,7 @@ def cpu_baseline_ml(calls, frames):
 
 def cpu_baseline(variant, calls, frames):
     """The oracle (CPU restatement of the whole adaptive path, oracle/bsa_oracle.py) timed on
-    this host's cores on a bounded sample: 2 heads of one attention call at the full sequence
+    this host's cores on a bounded sample: half the heads of one attention call (about 10 s) at the full sequence
     length, scaled to a whole video's calls. Baseline only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import bsa_oracle as O
