@@ -374,13 +374,13 @@ def cpu_baseline_ml(calls, frames):
 
 def cpu_baseline(variant, calls, frames):
     """The oracle (CPU restatement of the whole adaptive path, oracle/bsa_oracle.py) timed on
-    this host's cores on a bounded sample: half the heads of one attention call (about 10 s) at the full sequence
+    this host's cores on a bounded sample: a sixth (cog) or a quarter (wan) of the heads of one attention call at the full sequence
     length, scaled to a whole video's calls. Baseline only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import bsa_oracle as O
     cfg = O.AdaptiveConfig.cogvideox() if variant == "cog" else O.AdaptiveConfig.wan()
     V = VARIANTS[variant]
-    heads = 24 if variant == "cog" else 6   # about 10 s of CPU work (half of one call's heads)
+    heads = 8 if variant == "cog" else 3   # about 10 s of CPU work on the GPU box host
     L = cfg.width * cfg.height * cfg.depth + cfg.text_length
     g = torch.Generator().manual_seed(0)
     cent = torch.randn(1, heads, L // 128 + 1, V["D"], generator=g).repeat_interleave(128, 2)[:, :, :L]
