@@ -44,7 +44,7 @@ template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
 #endif
 template <int D> constexpr int kPBufs = VB_PRED_BUFS;
 #ifndef VB_FUSED_POOL_WGS
-#define VB_FUSED_POOL_WGS 256   // workgroups of the predictor's launch that run the pooled K/V pass
+#define VB_FUSED_POOL_WGS 512   // workgroups of the predictor's launch that run the pooled K/V pass
 #endif
 constexpr int kFusedPoolWgs = VB_FUSED_POOL_WGS;
 
