@@ -43,6 +43,10 @@ template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
 #define VB_PRED_MIN_WG 2
 #endif
 template <int D> constexpr int kPBufs = VB_PRED_BUFS;
+#ifndef VB_PRED_GATHER
+#define VB_PRED_GATHER 1   // K rows gathered by the score kernel's DMA (no sampled-row copy)
+#endif
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 #ifndef VB_FUSED_POOL_WGS
 #define VB_FUSED_POOL_WGS 512   // workgroups of the predictor's launch that run the pooled K/V pass
 #endif
@@ -233,6 +237,10 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
   const int b = bh / p.H, h = bh % p.H;
   int pos = min((jt >> 5) * p.block + koff[jt & 31], p.L - 1);
   if (p.rows) pos = p.rows[pos];
+  if (VB_PRED_GATHER) {   // the score kernel gathers the rows: only their byte offsets in the (b,h) slice
+    reinterpret_cast<int32_t*>(p.k_s)[(int64_t)bh * p.nb * 32 + jt] = (int32_t)((int64_t)pos * p.ks[2] * 2);
+    return;
+  }
   const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(p.k) +
                                                     2 * (b * p.ks[0] + h * p.ks[1] + (int64_t)pos * p.ks[2]));
   u32x4* dst = reinterpret_cast<u32x4*>(p.k_s + ((int64_t)bh * p.nb * 32 + jt) * p.D * 2);
@@ -290,7 +298,9 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   const int bh = lin / nqg;
   const int qb = (lin % nqg) * kPWaves + wave;  // this wave's sampled q-block
   const bool wave_active = qb < nb;
+#if !VB_PRED_GATHER
   const int64_t slice = (int64_t)nb * 32 * kRowB;   // bytes of one (b,h) sampled stream
+#endif
 
   // Q fragment of this lane's sampled row (B operand of S^T = K_s . Q_s^T), gathered straight from
   // the caller's q: reordered-padded position qb*block + q_off[l32] (replicate padding) at row rows[pos]
@@ -308,6 +318,29 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // K tiles by LDS-DMA from the contiguous sampled stream: a buffer descriptor per (b,h), each
   // lane's fixed (row, swizzled chunk) as voffset, the tile's first row as soffset. Rows past the
   // stream (a partial last tile) read as zeros and are never used.
+#if VB_PRED_GATHER
+  // Gather mode: the sampling launch wrote only the byte offsets of the sampled rows within the
+  // (b,h) slice of k (int32 table [bh][nb*32]); K tiles are gathered straight from k. Per tile each
+  // wave DMAs the offsets of its own rows into a small LDS ring two tiles ahead (one 4-byte lane
+  // each, ordered so that lane L's four rows are 16 contiguous bytes), reads them back and issues
+  // the row DMAs with per-lane voffsets. 27 MB of row copies per CogVideoX call are not made.
+  static_assert(kBufs == 3, "the gather pipeline's vmcnt counts assume a 3-slot K ring");
+  constexpr int kChunks = kRowB / 16;
+  const uint8_t* kslice = reinterpret_cast<const uint8_t*>(p.k) + 2 * ((bh / p.H) * p.ks[0] + (bh % p.H) * p.ks[1]);
+  const srd_t ksrd = make_srd(kslice, (int)((int64_t)(p.L - 1) * p.ks[2] * 2 + kRowB));
+  const srd_t isrd = make_srd(reinterpret_cast<const int32_t*>(p.k_s) + (int64_t)bh * nb * 32, nb * 32 * 4);
+  uint8_t* ibuf = ktile + kBufs * kTileBytes + wave * 256;   // [4 tiles][4 waves][64 dwords]
+  int cv[kInstPerWave];   // the lane's swizzled chunk within its row, per DMA instruction
+#pragma unroll
+  for (int i = 0; i < kInstPerWave; ++i) {
+    const int r = (wave * kInstPerWave + i) * kRowsPerInst + lane / kChunks;
+    const int sw = (D == 64) ? ((r >> 1) & 7) : (r & 15);
+    cv[i] = 16 * ((lane % kChunks) ^ sw);
+  }
+  // offset-DMA lane 4j + i fetches row (wave*kIPW + i)*kRowsPerInst + j of the tile (lanes past the
+  // wave's rows repeat the last one)
+  const int ivoff = 4 * ((wave * kInstPerWave + (lane & 3)) * kRowsPerInst + min(lane >> 2, kRowsPerInst - 1));
+#else
   const srd_t ksrd = make_srd(p.k_s + bh * slice, (int)slice);
   int voff[kInstPerWave];
 #pragma unroll
@@ -317,6 +350,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
     const int sw = (D == 64) ? ((r >> 1) & 7) : (r & 15);
     voff[i] = r * kRowB + 16 * (sl ^ sw);
   }
+#endif
   float m = -INFINITY;
   __syncthreads();   // all plain global loads retired before the DMA pipeline
 
@@ -324,12 +358,30 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // K tile t by LDS-DMA (global_load_lds_dwordx4): the LDS image is written linearly (1 KiB per
   // wave-instruction), so the 16-byte-chunk XOR swizzle of the image is applied to each lane's
   // SOURCE address: LDS slot `sl` of row r holds chunk sl ^ sw(r).
+#if VB_PRED_GATHER
+  // offsets of tile t's rows -> LDS ring slot t & 3 (one instruction per wave; past the table: 0).
+  // Four slots: the prologue has I0..I2 in flight at once, a body reads I(t+2) while I(t+3) lands.
+  auto issue_idx = [&](int t) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(isrd.base), (short)0, isrd.bytes, 0x00020000),
+        (__attribute__((address_space(3))) void*)(ibuf + (t & 3) * (kPWaves * 256)), 4, ivoff,
+        __builtin_amdgcn_readfirstlane(t * kKeysPerTile<D> * 4), 0, 0);
+  };
+  // rows of tile t (offsets already in LDS) -> K ring slot t % kBufs
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    uint8_t* dst = ktile + (t % kBufs) * kTileBytes;
+    const i32x4 o = *reinterpret_cast<const i32x4*>(ibuf + (t & 3) * (kPWaves * 256) + 16 * (lane / kChunks));
+#pragma unroll
+    for (int i = 0; i < kInstPerWave; ++i) dma16(ksrd, dst + (wave * kInstPerWave + i) * 1024, o[i] + cv[i], 0);
+  };
+#else
   auto issue = [&](int t) __attribute__((always_inline)) {
     uint8_t* dst = ktile + (t % kBufs) * kTileBytes;
 #pragma unroll
     for (int i = 0; i < kInstPerWave; ++i)
       dma16(ksrd, dst + (wave * kInstPerWave + i) * 1024, voff[i], t * kTileBytes);
   };
+#endif
   // loop-invariant lane addresses of the K fragment reads (the swizzle depends on the lane's row
   // bits only), so every read of every slot is base + compile-time immediate
   int k_lane[KS];
@@ -340,9 +392,35 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   }
   uint16_t* Rq = p.rbuf + ((int64_t)bh * nb + (wave_active ? qb : 0)) * nb * 32;   // this q-block
   const srd_t rsrd = make_srd(Rq, wave_active ? nb * 64 : 0);
+#if VB_PRED_GATHER
+  // Issue order: I0 I1 I2 K0 K1, then per body t: I(t+3) K(t+2) [compute] S(t) — every DMA is
+  // issued, past the last tile too (offsets past the table read 0: row 0 into a slot no tile reads
+  // any more), so the counts below are constant. Body t needs K(t) and I(t+2); younger than I(t+2)
+  // are K(t+1) and S(t-1) (for t = 0: only K1), so K(t+1) stays in flight.
+  if (ntiles > 0) {
+    issue_idx(0);
+    issue_idx(1);
+    issue_idx(2);
+    VB_WAIT_VMCNT(2);
+    asm volatile("" ::: "memory");   // the offsets' LDS reads stay behind the wait
+    issue(0);
+    VB_WAIT_VMCNT(1 + kInstPerWave);
+    asm volatile("" ::: "memory");
+    issue(1);
+  }
+#else
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
+#endif
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
+#if VB_PRED_GATHER
+    if (t == 0) VB_WAIT_VMCNT(kInstPerWave);
+    else VB_WAIT_VMCNT(kInstPerWave + kSt);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue_idx(t + 3);
+    issue(t + 2);
+#else
     // retire this wave's DMA of tile t, then the barrier makes every wave's part visible and
     // guarantees tile t-1's buffer is no longer being read. vmcnt counts the R stores too, in issue
     // order: younger than DMA(t) are the stores of the (up to kBufs-1) bodies since it was issued
@@ -354,6 +432,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
     else wait_vmcnt_upto<kBufs * kSt + kBufs * kInstPerWave>(nst * kSt + ndma * kInstPerWave);
     __builtin_amdgcn_s_barrier();
     if (t + kBufs - 1 < ntiles) issue(t + kBufs - 1);
+#endif
     const uint8_t* kl = ktile + u * kTileBytes;
     if (VB_DIAG && (p.dbg & 4)) return;   // diagnostic: stream the K tiles only
     // one accumulator per 32-key block: the MFMAs of block kt+1 do not wait for the row-max
@@ -423,6 +502,9 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
       if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
   }
   static_assert(kBufs >= 2 && kBufs <= 4, "the loop body is instantiated once per ring slot");
+#if VB_PRED_GATHER
+  VB_WAIT_VMCNT(0);   // the DMAs issued past the last tile land before the epilogue reuses the LDS
+#endif
   m = max_xor32(m);   // the two halves saw alternate key blocks
   if (half == 0) mrow_s[wave * 32 + l32] = m;
   __syncthreads();
@@ -515,13 +597,14 @@ static size_t predict_smem_bytes(int nb, int D) {
   const size_t tiles = D == 64 ? (size_t)kPBufs<64> * kKeysPerTile<64> * 64 * 2
                                : (size_t)kPBufs<128> * kKeysPerTile<128> * 128 * 2;
   const size_t scratch = (size_t)kPWaves * 2 * (kMaxNb + 4) * 4;
-  return kPWaves * 32 * 4 + (tiles > scratch ? tiles : scratch);
+  const size_t ring = VB_PRED_GATHER ? 4 * kPWaves * 256 : 0;   // gather mode: the row-offset ring
+  return kPWaves * 32 * 4 + (tiles + ring > scratch ? tiles + ring : scratch);
 }
 
-// workspace: sampled k rows | R
+// workspace: sampled k rows (gather mode: their int32 byte offsets) | R
 static uint64_t predict_rows_bytes(int B, int H, int L, int D) {
   const int nb = (L + 127) / 128;
-  return (uint64_t)B * H * nb * 32 * D * 2;
+  return (uint64_t)B * H * nb * 32 * (VB_PRED_GATHER ? 4 : D * 2);
 }
 static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
   const uint64_t nb = (L + 127) / 128;
@@ -575,6 +658,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
     return fail(VB_ERR_INVALID, "vb_mask_predict: workspace missing or smaller than vb_mask_predict_workspace_size()");
   const uint64_t rows_b = predict_rows_bytes(a->B, a->H, a->L, a->D);
   if (rows_b / a->B / a->H >= (uint64_t(1) << 31)) return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: sampled stream too large");
+  if ((int64_t)(a->L - 1) * a->k_stride[2] * 2 + 2 * a->D >= (int64_t(1) << 31))
+    return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: a k (b,h) slice spans >= 2 GiB");
   for (int i = 0; i < 3; ++i)
     if ((a->q_stride[i] | a->k_stride[i]) & 7) return fail(VB_ERR_INVALID, "vb_mask_predict: strides must be multiples of 8");
   PredParams p{};
