@@ -47,6 +47,9 @@ template <int D> constexpr int kPBufs = VB_PRED_BUFS;
 #define VB_PRED_GATHER 1   // K rows gathered by the score kernel's DMA (no sampled-row copy)
 #endif
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+#ifndef VB_FUSED_POOL_LAST
+#define VB_FUSED_POOL_LAST 0   // 1: pooling workgroups after the score workgroups (measured 1-4 % slower)
+#endif
 #ifndef VB_FUSED_POOL_WGS
 #define VB_FUSED_POOL_WGS 512   // workgroups of the predictor's launch that run the pooled K/V pass
 #endif
@@ -276,11 +279,21 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // The first n_pool workgroups of the launch run the pooled K/V pass (HBM-bound) beside the score
   // workgroups (MFMA-bound): one launch, no second stream or events. n_pool is a multiple of 8, so
   // the score workgroups keep their XCD (blockIdx % 8).
+#if VB_FUSED_POOL_LAST
+  // pooling workgroups after the score workgroups: they fill the score kernel's last, partial round
+  const int n_score = (int)gridDim.x - p.n_pool;
+  if ((int)blockIdx.x >= n_score) {
+    pool_kv_span<T>(p.pool, (int64_t)((int)blockIdx.x - n_score) * blockDim.x + threadIdx.x, (int64_t)p.n_pool * blockDim.x);
+    return;
+  }
+  const int wg = (int)blockIdx.x;
+#else
   if ((int)blockIdx.x < p.n_pool) {
     pool_kv_span<T>(p.pool, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)p.n_pool * blockDim.x);
     return;
   }
   const int wg = (int)blockIdx.x - p.n_pool;
+#endif
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nb = p.nb;
   float* mrow_s = reinterpret_cast<float*>(smem);
