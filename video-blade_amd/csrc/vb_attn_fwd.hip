@@ -488,11 +488,11 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     // WITHOUT overwriting S; returns the lane's fp32 sum (four independent chains)
     auto exp_pack = [&](const f32x16& x, typename T::vec8& p0, typename T::vec8& p1) __attribute__((always_inline)) -> float {
       float e[16];
-      float h4[4] = {0.f, 0.f, 0.f, 0.f};
+      float h4[4];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         e[r] = exp2_fast(x[r]);
-        h4[r & 3] += e[r];
+        h4[r & 3] = r < 4 ? e[r] : h4[r & 3] + e[r];   // chains start at their first value (no 0 + e)
       }
       u32x4 u0, u1;
 #pragma unroll
@@ -693,7 +693,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
         for (int r = 0; r < 16; ++r) {
           const float e = exp2_fast(kCBias ? s[kt][r] : fmaf(s[kt][r], p.c, nbias));
           s[kt][r] = e;
-          lq[(2 * kt + r) & 3] += e;
+          lq[(2 * kt + r) & 3] = (kt == 0 && r < 4) ? e : lq[(2 * kt + r) & 3] + e;   // no 0 + e
         }
 #pragma unroll
         for (int kk = 2 * kt; kk < 2 * kt + 2; ++kk) {
@@ -713,7 +713,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
         for (int r = 0; r < 16; ++r) {
           const float e = exp2_fast(kCBias ? s[kt][r] : fmaf(s[kt][r], p.c, nbias));
           s[kt][r] = e;
-          lq[(2 * kt + r) & 3] += e;
+          lq[(2 * kt + r) & 3] = (kt == 0 && r < 4) ? e : lq[(2 * kt + r) & 3] + e;
         }
       ls = (lq[0] + lq[1]) + (lq[2] + lq[3]);
     }
