@@ -20,6 +20,9 @@ KERNELS = [
     "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb1EEEvNS_9FwdParamsE",
     "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb0EEEvNS_9FwdParamsE",
     "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb0EEEvNS_9FwdParamsE",
+    # the module's path: K/V rows gathered through the Gilbert index
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb1ELb0ELb1EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb1ELb0ELb1EEEvNS_9FwdParamsE",
 ]
 
 

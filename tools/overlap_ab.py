@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
-"""A/B: the pooled K/V pass on a side stream (overlap=True) vs in order on the caller's stream."""
+"""A/B of a boolean module option in one process (default: overlap; --opt gather_kv)."""
 import os
 import statistics
 import sys
 
 import torch
+
+OPT = sys.argv[sys.argv.index('--opt') + 1] if '--opt' in sys.argv else 'overlap'
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
@@ -15,7 +17,7 @@ from bench import realistic_qkv  # noqa: E402
 dev = torch.device("cuda")
 for variant in ("cog", "wan"):
     H, D = (48, 64) if variant == "cog" else (12, 128)
-    mods = {ov: vblade.AdaptiveBlockSparseAttn(variant, log_every=0, overlap=ov) for ov in (True, False)}
+    mods = {ov: vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **{OPT: ov}) for ov in (True, False)}
     L = mods[True].gilbert_rearranger.seq_len
     q, k, v = realistic_qkv(H, L, D, 0, dev)
     times = {True: [], False: []}
@@ -34,4 +36,4 @@ for variant in ("cog", "wan"):
                 torch.cuda.synchronize()
                 times[ov].append(e0.elapsed_time(e1) / 10)
     for ov in (True, False):
-        print(f"{variant} overlap={ov}: median {statistics.median(times[ov]):.4f} ms/call", flush=True)
+        print(f"{variant} {OPT}={ov}: median {statistics.median(times[ov]):.4f} ms/call", flush=True)

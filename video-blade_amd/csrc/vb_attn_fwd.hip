@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   constexpr int kRowsPerInst = 1024 / kRowB;   // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerMat = kMatBytes / 1024;
   constexpr int kInstPerWave = 2 * kInstPerMat / 4;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kBufs * kBufBytes + kMaxBlocks * 2 + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kBufs * kBufBytes + kMaxBlocks * 2 + 16 + (kKvRows ? 4 * 512 : 0)];
   static_assert(!(kML && (kPool || kKvRows)), "multi-level mode reads the KV pyramids only");
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
   int* list_n = reinterpret_cast<int*>(smem + kBufs * kBufBytes + kMaxBlocks * 2);
@@ -337,12 +337,18 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   const int src_rows = kML ? 15 * (p.Lpad / 8) : Lk;   // pyramid rows in multi-level mode
   const srd_t my_rsrc = make_srd(my_base, p.use_main ? (int)((int64_t)(src_rows - 1) * my_stride + kRowB) : 0);
   const srd_t my_prsrc = make_srd(kPool ? my_pbase : my_base, kPool ? (int)((int64_t)(p.Lkp - 1) * my_pstride + kRowB) : 0);
-  int my_voff[kInstPerWave], my_pvoff[kInstPerWave];
+  // multi-level: per-lane voffsets, rows relative to the instruction's 16-row quarter (its start
+  // is the soffset). Otherwise only the swizzled chunk is kept per instruction: instruction i's
+  // row is my_row0 + i*kRowsPerInst, so its voffset is my_row0*rowb + chunk (one VALU per tile and
+  // instruction) and the i*kRowsPerInst*rowb part goes to the scalar soffset. Fewer live VGPRs
+  // than one offset per instruction and key source (a spilled one stalled the D=128 DMA ring).
+  int my_voff[kInstPerWave];
+  int my_rc[kInstPerWave];
+  const int my_row0 = my_row[0];
 #pragma unroll
   for (int i = 0; i < kInstPerWave; ++i) {
-    // multi-level: rows relative to the instruction's 16-row quarter (its start is the soffset)
-    my_voff[i] = (kML ? (my_row[i] & 15) : my_row[i]) * my_rowb + my_chunk[i] * 16;
-    my_pvoff[i] = my_row[i] * my_prowb + my_chunk[i] * 16;
+    my_rc[i] = my_chunk[i] * 16;
+    if constexpr (kML) my_voff[i] = (my_row[i] & 15) * my_rowb + my_chunk[i] * 16;
   }
   auto ml_issue = [&](const MlTileSrc src, int slot) __attribute__((always_inline)) {
     uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
@@ -352,31 +358,61 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     for (int i = 0; i < kInstPerWave; ++i)
       dma16(my_rsrc, dst + i * 1024, my_voff[i], (i * kRowsPerInst >= 16) ? soffB : soffA);
   };
-  auto issue = [&](const TileSrc src, int slot) __attribute__((always_inline)) {
+  // Gathered K/V rows (kv_rows: reordered key -> caller row; the module's path on the caller's own
+  // k/v). Per tile every wave DMAs the kv_rows entries of its own 32 rows into a 4-slot LDS ring
+  // one DMA stage ahead of the rows themselves (lane 32 lanes, entry j*kIPW + i = the row of DMA
+  // instruction i for lanes with row j), reads its kIPW entries back with one or two ds_read_b128
+  // and issues the row DMAs with per-lane voffsets row * stride + chunk (v_mad_u32_u24). Every
+  // body issues one offset DMA and kIPW row DMAs, past the last tile too, so the vmcnt counts are
+  // constants (see the body).
+  const int gather_key = ((wave & 1) * kInstPerWave + (lane % kInstPerWave)) * kRowsPerInst + lane / kInstPerWave;
+  const srd_t rows_srd = make_srd(kKvRows ? p.kv_rows : nullptr, kKvRows ? Lk * 4 : 0);
+  uint8_t* const ibase = smem + kBufs * kBufBytes + kMaxBlocks * 2 + 16 + wave * 128;   // [4][4 waves][32]
+  auto issue_idx = [&](int t, int blk_raw) __attribute__((always_inline)) {
+    int voff = 0;   // pooled tiles and tiles past the end: a harmless entry
+    if (t < ntm) {
+      const int kstart = __builtin_amdgcn_readfirstlane(blk_raw) * kQBlk + (t & 1) * kKT;
+      voff = 4 * (kstart + min(gather_key, min(kKT, Lk - kstart) - 1));
+    }
+    if (lane < 32)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(rows_srd.base), (short)0, rows_srd.bytes, 0x00020000),
+          (__attribute__((address_space(3))) void*)(ibase + (t & 3) * 512), 4, voff, 0, 0, 0);
+  };
+  auto issue = [&](const TileSrc src, int slot, int t = 0) __attribute__((always_inline)) {
     uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
     const bool pooled = kPool && src.pooled;
-    if (kKvRows && !pooled) {   // gathered k/v rows (generic API path; serialises the ring)
+    if (kKvRows && !pooled) {
+      typedef int i32x4 __attribute__((ext_vector_type(4)));
+      int o[kInstPerWave];
+      const uint8_t* ib = ibase + (t & 3) * 512 + 4 * kInstPerWave * (lane / kChunks);
+#pragma unroll
+      for (int c = 0; c < kInstPerWave; c += 4) {
+        const i32x4 w = *reinterpret_cast<const i32x4*>(ib + 4 * c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[c + e] = w[e];
+      }
 #pragma unroll
       for (int i = 0; i < kInstPerWave; ++i) {
-        int key = src.kstart + min(my_row[i], src.klen - 1);
-        key = p.kv_rows[key];
-        const uint8_t* gsrc = my_base + (int64_t)key * my_stride + my_chunk[i] * 16;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                         (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+        int voff;   // row * stride + chunk: rows < 2^24 and strides < 2^24 bytes (host-checked)
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(voff) : "v"(o[i]), "s"(my_rowb), "v"(my_chunk[i] * 16));
+        dma16(my_rsrc, dst + i * 1024, voff, 0);
       }
       return;
     }
     const int rowb = pooled ? my_prowb : my_rowb;
     const int soff = __builtin_amdgcn_readfirstlane(src.kstart * rowb);
     if (src.klen == kKT) {
+      const int vb0 = my_row0 * rowb;
 #pragma unroll
       for (int i = 0; i < kInstPerWave; ++i)
-        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, pooled ? my_pvoff[i] : my_voff[i], soff);
+        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, vb0 + my_rc[i],
+              __builtin_amdgcn_readfirstlane(soff + i * kRowsPerInst * rowb));
     } else {   // tail tile: clamp rows to the last valid key (replicated rows are masked later)
 #pragma unroll
       for (int i = 0; i < kInstPerWave; ++i) {
-        const int r = min(my_row[i], src.klen - 1);
-        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, r * rowb + my_chunk[i] * 16, soff);
+        const int r = min(my_row0 + i * kRowsPerInst, src.klen - 1);
+        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, r * rowb + my_rc[i], soff);
       }
     }
   };
@@ -757,13 +793,33 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     else issue(src, slot);
   };
   Src slot_src[kBufs];
-  slot_src[0] = any_tile_src(0, any_list_at(0));
-  if (ntiles > 0) any_issue(slot_src[0], 0);
-  if constexpr (kBufs > 2) {
-    slot_src[1] = any_tile_src(1, any_list_at(1));
-    if (ntiles > 1) any_issue(slot_src[1], 1);
+  int next_blk, idx_blk = 0;
+  if constexpr (kKvRows) {
+    // I0 .. I(kBufs-1), then the rows of tiles 0 .. kBufs-2, each once its offsets have landed
+    // (younger than I(s): I(s+1) .. I(kBufs-1) and the s row stages already issued)
+#pragma unroll
+    for (int s0 = 0; s0 < kBufs; ++s0) issue_idx(s0, list_at(s0));
+    slot_src[0] = tile_src(0, list_at(0));
+    VB_WAIT_VMCNT(kBufs - 1);
+    asm volatile("" ::: "memory");
+    issue(slot_src[0], 0, 0);
+    if constexpr (kBufs > 2) {
+      slot_src[1] = tile_src(1, list_at(1));
+      VB_WAIT_VMCNT(kBufs - 2 + kInstPerWave);
+      asm volatile("" ::: "memory");
+      issue(slot_src[1], 1, 1);
+    }
+    next_blk = list_at(kBufs - 1);
+    idx_blk = list_at(kBufs);
+  } else {
+    slot_src[0] = any_tile_src(0, any_list_at(0));
+    if (ntiles > 0) any_issue(slot_src[0], 0);
+    if constexpr (kBufs > 2) {
+      slot_src[1] = any_tile_src(1, any_list_at(1));
+      if (ntiles > 1) any_issue(slot_src[1], 1);
+    }
+    next_blk = any_list_at(kBufs - 1);
   }
-  int next_blk = any_list_at(kBufs - 1);
   // The loop body is instantiated once per ring slot (compile-time U), so every LDS address is a
   // loop-invariant lane base + immediate offset: no address VALU inside the loop.
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
@@ -772,20 +828,35 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     VB_STAMP(st0);
     // retire this wave's DMAs of tile t (younger tiles stay in flight); the barrier then makes
     // every wave's part visible and proves slot (t-1) % kBufs is no longer being read
-    const int younger = min(ntiles - 1 - t, kBufs - 2);
-    if (younger >= 2) VB_WAIT_VMCNT(2 * kInstPerWave);
-    else if (younger == 1) VB_WAIT_VMCNT(kInstPerWave);
-    else VB_WAIT_VMCNT(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    const int ti = t + kBufs - 1;
+    if constexpr (kKvRows) {
+      // per body: I(t+kBufs) then the rows of tile t+kBufs-1, always (past the end too). Body t
+      // needs K/V(t) and I(t+kBufs-1); only the rows of tile t+1 (3-slot ring) are younger.
+      if constexpr (kBufs == 3) VB_WAIT_VMCNT(kInstPerWave);
+      else VB_WAIT_VMCNT(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue_idx(t + kBufs, idx_blk);
+      slot_src[un] = tile_src(ti, next_blk);
+      issue(slot_src[un], un, ti);
+      next_blk = idx_blk;
+      idx_blk = list_at(t + kBufs + 1);   // in flight during this tile's compute
+    } else {
+      const int younger = min(ntiles - 1 - t, kBufs - 2);
+      if (younger >= 2) VB_WAIT_VMCNT(2 * kInstPerWave);
+      else if (younger == 1) VB_WAIT_VMCNT(kInstPerWave);
+      else VB_WAIT_VMCNT(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (ti < ntiles) {
+        slot_src[un] = any_tile_src(ti, next_blk);
+        any_issue(slot_src[un], un);
+        next_blk = any_list_at(ti + 1);   // in flight during this tile's compute
+      }
+    }
     VB_STAMP(st1);
     VB_ACC(0, st1 - st0);
-    const int ti = t + kBufs - 1;
-    if (ti < ntiles) {
-      slot_src[un] = any_tile_src(ti, next_blk);
-      any_issue(slot_src[un], un);
-      next_blk = any_list_at(ti + 1);   // in flight during this tile's compute
-    }
     VB_STAMP(st2);
     VB_ACC(1, st2 - st1);
     const Src src = slot_src[u];
@@ -803,6 +874,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     if constexpr (kBufs > 2)
       if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
   }
+  if constexpr (kKvRows) VB_WAIT_VMCNT(0);   // the stages issued past the last tile land before exit
 #if VB_DIAG
   if (lane == 0) {
     for (int i = 0; i < 5; ++i) atomicAdd(&g_vb_stamp[i], acc_st[i]);
@@ -854,8 +926,12 @@ template <int D, class T>
 static int launch_fwd(const FwdParams& p, bool pool, hipStream_t stream) {
   const dim3 grid(p.nbq * p.B * p.H);
   const bool rows = p.kv_rows != nullptr;
-  const bool cbias = VB_FWD_CBIAS && p.lse == nullptr && !rows;
-  if (cbias && pool)
+  const bool cbias = VB_FWD_CBIAS && p.lse == nullptr;
+  if (cbias && pool && rows)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, true, false, true>), grid, dim3(kThreads), 0, stream, p);
+  else if (cbias && rows)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, true, false, true>), grid, dim3(kThreads), 0, stream, p);
+  else if (cbias && pool)
     hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, false, false, true>), grid, dim3(kThreads), 0, stream, p);
   else if (cbias)
     hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, false, false, true>), grid, dim3(kThreads), 0, stream, p);
@@ -917,6 +993,8 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
     if (a->use_main && ((a->k_stride[i] | a->v_stride[i]) & 7)) return fail(VB_ERR_INVALID, "vb_attn_fwd: k/v strides must be multiples of 8 elements");
     if (pool && ((a->kp_stride[i] | a->vp_stride[i]) & 7)) return fail(VB_ERR_INVALID, "vb_attn_fwd: kp/vp strides must be multiples of 8 elements");
   }
+  if (a->kv_rows && (a->Lk >= (1 << 24) || a->k_stride[2] * 2 >= (1 << 24) || a->v_stride[2] * 2 >= (1 << 24)))
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: kv_rows needs Lk and the k/v row strides (bytes) < 2^24");
   const int64_t kLim = int64_t(1) << 31;   // one (b,h) slice must be addressable by a 32-bit buffer offset
   if (a->use_main && ((int64_t)(a->Lk - 1) * 2 * (a->k_stride[2] > a->v_stride[2] ? a->k_stride[2] : a->v_stride[2]) + 2 * a->D >= kLim))
     return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: a k/v (b,h) slice spans >= 2 GiB");

@@ -116,7 +116,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
         if variant not in VARIANT_DEFAULTS:
             raise ValueError(f"variant must be one of {list(VARIANT_DEFAULTS)}")
         cfg = dict(VARIANT_DEFAULTS[variant])
-        unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep", "overlap"}
+        unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep", "overlap", "gather_kv"}
         if unknown:
             raise TypeError(f"unknown options {sorted(unknown)}")
         cfg.update(overrides)
@@ -147,6 +147,12 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self.attn_events: Optional[list] = None
         # overlap the pooled K/V pass with the predictor on a second stream (inference only)
         self.overlap = bool(cfg.get("overlap", True))
+        # The attention kernel gathers K/V rows through the Gilbert index (True) or streams the
+        # Gilbert-ordered contiguous copies the pooled pass writes (False: 2·L·D·2 bytes more per
+        # head, written beside the predictor). "auto" (default) takes what measured faster per
+        # head dim (tools/overlap_ab.py --opt gather_kv): gather at D=128 (Wan, +2.4 % per call),
+        # copies at D=64 (CogVideoX, +0.9 %).
+        self.gather_kv = cfg.get("gather_kv", "auto")
         self._side = ops.SideStream()
 
     # -------------------------------------------------------------------------------- helpers
@@ -227,19 +233,22 @@ class AdaptiveBlockSparseAttn(nn.Module):
             # predictor's score-kernel launch, beside the MFMA-bound score workgroups (overlap=True),
             # or after it (overlap=False)
             ride = fused and self.overlap
-            outs = ops.pool_kv_outputs(k, self.sample_gap, reordered=True) if ride else None
+            gather = (D == 128) if self.gather_kv == "auto" else bool(self.gather_kv)
+            copies = not (gather and rows is not None)
+            outs = ops.pool_kv_outputs(k, self.sample_gap, reordered=copies) if ride else None
             with torch.no_grad():
                 _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count,
                                             pool=(v, self.sample_gap, outs) if ride else None)
             if ride:
                 pooled = outs
             elif fused:
-                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True)
+                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=copies)
         else:
             mask = block_mask.to(torch.uint8)
             count.add_(mask.sum())
             if fused:
-                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=True)
+                gather = (D == 128) if self.gather_kv == "auto" else bool(self.gather_kv)
+                pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=not (gather and rows is not None))
         self._slot_totals.append(B * H * nb * nb)
         self.sparsity_counter += 1
         self.last_mask = mask
@@ -248,13 +257,18 @@ class AdaptiveBlockSparseAttn(nn.Module):
             out = adaptive_split_attention(q, k, v, mask, rows, self.sample_gap)
         else:
             # q rows gathered and out rows scattered inside the attention kernel
-            kp, vp, k_r, v_r = pooled
+            if len(pooled) == 4:   # Gilbert-ordered copies: streamed contiguously
+                kp, vp, k_src, v_src = pooled
+                kv_rows = None
+            else:                  # the caller's k/v, rows gathered through the Gilbert index
+                kp, vp = pooled
+                k_src, v_src, kv_rows = k, v, rows
             ev = self.attn_events
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            out = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
-                                    kp_log_bias=math.log(self.sample_gap),
+            out = ops.attention_fwd(q, k_src, v_src, block_mask=mask, q_rows=rows, kv_rows=kv_rows,
+                                    kp=kp, vp=vp, kp_log_bias=math.log(self.sample_gap),
                                     heavy_rows=self.force_tail)
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
