@@ -32,6 +32,9 @@ namespace vb {
 #ifndef VB_LAZY_NOCHECK
 #define VB_LAZY_NOCHECK 0   // diagnostic builds only: no overflow check (timing of the fast path alone)
 #endif
+#ifndef VB_NODMA
+#define VB_NODMA 0   // diagnostic: tiles past the first ring fill are not loaded (stale LDS)
+#endif
 #if VB_DIAG || VB_LAZY_COUNT
 __device__ unsigned long long g_vb_stamp[16];
 #endif
@@ -851,7 +854,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       __builtin_amdgcn_s_barrier();
       if (ti < ntiles) {
         slot_src[un] = any_tile_src(ti, next_blk);
-        any_issue(slot_src[un], un);
+        if (!(VB_NODMA && ti >= kBufs)) any_issue(slot_src[un], un);   // VB_NODMA: timing diagnostic only
         next_blk = any_list_at(ti + 1);   // in flight during this tile's compute
       }
     }
