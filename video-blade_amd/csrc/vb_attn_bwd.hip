@@ -589,9 +589,13 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
   constexpr int kCh = RB / 16;
   constexpr int kInst = 2 * kInstTile;
   constexpr int kBufBytes = 2 * kTileBytes;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBufBytes + kMaxBlocks * 2 + 16];
-  uint16_t* list = reinterpret_cast<uint16_t*>(smem + 2 * kBufBytes);
-  int* list_n = reinterpret_cast<int*>(smem + 2 * kBufBytes + kMaxBlocks * 2);
+  // D=128: 3-slot K/V ring, tile t is read while t+1 and t+2 are in flight, and one barrier per
+  // tile both publishes tile t and proves slot (t-1) % 3 free for tile t+2 (+2 % on Wan's backward).
+  // D=64: 2 slots and a second barrier per tile (the 3-slot form measured 1 % slower there).
+  constexpr int kRing = D == 128 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * kBufBytes + kMaxBlocks * 2 + 16];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + kRing * kBufBytes);
+  int* list_n = reinterpret_cast<int*>(smem + kRing * kBufBytes + kMaxBlocks * 2);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -760,7 +764,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
       tile_keys(t, kstart, klen);
     }
     const bool pooled = kPool && t >= ntm;
-    uint8_t* buf = smem + (t & 1) * kBufBytes;
+    uint8_t* buf = smem + (kRing == 2 ? (t & 1) : t % kRing) * kBufBytes;
     for (int i = wave; i < kInst; i += 4) {
       const bool isv = i >= kInstTile;
       const int ii = isv ? i - kInstTile : i;
@@ -785,15 +789,18 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
   const bool many = wave < (kInst & 3);
 
   if (ntiles > 0) issue(0);
+  if (kRing == 3 && ntiles > 1) issue(1);
   for (int t = 0; t < ntiles; ++t) {
+    if (kRing == 2 && t + 1 < ntiles) issue(t + 1);
+    // retire this wave's part of tile t (tile t+1's stays in flight), then the barrier
     if (t + 1 < ntiles) {
-      issue(t + 1);
       if (many) VB_WAIT_VMCNT(kHi);
       else VB_WAIT_VMCNT(kLo);
     } else {
       VB_WAIT_VMCNT(0);
     }
     __builtin_amdgcn_s_barrier();
+    if (kRing == 3 && t + 2 < ntiles) issue(t + 2);
     int kstart, klen;
     float nL;
     bool pooled;
@@ -807,7 +814,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
       nL = -(pooled ? L2 : L1);
     }
     const float Dr = pooled ? D2 : D1;
-    const uint8_t* kt_ = smem + (t & 1) * kBufBytes;
+    const uint8_t* kt_ = smem + (kRing == 2 ? (t & 1) : t % kRing) * kBufBytes;
     const uint8_t* vt_ = kt_ + kTileBytes;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {   // 32-key halves: S^T, dP^T -> dS^T -> dQ^T
@@ -860,7 +867,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
         dq[j % DT] = T::mfma32(join8<T>(rk[sl][0], rk[sl][1]), pdv[j / DT], dq[j % DT]);
       }
     }
-    __builtin_amdgcn_s_barrier();
+    if (kRing == 2) __builtin_amdgcn_s_barrier();   // slot t % 2 is refilled by the next issue
   }
 
   if (!qvalid) return;
