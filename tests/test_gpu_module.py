@@ -177,3 +177,27 @@ def test_gathered_kv_rows_equal_gilbert_copies(variant, D):
     torch.cuda.synchronize()
     assert torch.equal(mods[0].last_mask, mods[1].last_mask)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("variant,D", [("cog", 64), ("wan", 128)])
+def test_module_takes_the_processors_strided_layout(variant, D):
+    """The diffusers processors hand inner_attention views `[B,L,H,D].transpose(1, 2)` (row stride
+    H*D, not D). Every kernel reads through strides (sampled rows, pooled pass, gathered K/V), so
+    the module's output on those views must equal its output on contiguous copies, bit for bit."""
+    import vblade
+    kw = dict(width=12, height=8, depth=6, text_length=26) if variant == "cog" else dict(width=13, height=6, depth=7)
+    m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **kw)
+    L = m.gilbert_rearranger.seq_len
+    H = 3
+    g = torch.Generator(device=DEV).manual_seed(33)
+    q, k, v = (torch.randn(1, L, H, D, generator=g, device=DEV).bfloat16().transpose(1, 2) for _ in range(3))
+    assert not q.is_contiguous()
+    outs, masks = [], []
+    with torch.no_grad():
+        for args in ((q, k, v), tuple(t.contiguous() for t in (q, k, v))):
+            torch.manual_seed(5)
+            outs.append(m(*args))
+            masks.append(m.last_mask.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(masks[0], masks[1])
+    assert torch.equal(outs[0], outs[1])
