@@ -201,3 +201,27 @@ def test_module_takes_the_processors_strided_layout(variant, D):
     torch.cuda.synchronize()
     assert torch.equal(masks[0], masks[1])
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("variant,D", [("cog", 64), ("wan", 128)])
+def test_batched_call_equals_per_sample_calls(variant, D):
+    """Classifier-free guidance runs the module on B=2 (and TDM training on B=5). With the same
+    sampled offsets, the batched call equals one call per batch element, bit for bit: the batch
+    index only selects slices (no cross-batch reduction anywhere on the path)."""
+    import vblade
+    from vblade import attention
+    kw = dict(width=12, height=8, depth=6, text_length=26) if variant == "cog" else dict(width=13, height=6, depth=7)
+    m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **kw)
+    L = m.gilbert_rearranger.seq_len
+    B, H = 2, 3
+    g = torch.Generator(device=DEV).manual_seed(44)
+    q, k, v = (torch.randn(B, H, L, D, generator=g, device=DEV).bfloat16() for _ in range(3))
+    q_off, k_off = attention.draw_sample_offsets_qk(B, H, DEV, generator=g)
+    with torch.no_grad():
+        out = m(q, k, v, q_off=q_off, k_off=k_off)
+        mask = m.last_mask.clone()
+        for b in range(B):
+            sl = slice(b, b + 1)
+            ob = m(q[sl], k[sl], v[sl], q_off=q_off[sl], k_off=k_off[sl])
+            assert torch.equal(m.last_mask, mask[sl])
+            assert torch.equal(ob, out[sl])
