@@ -222,7 +222,8 @@ def _exact_inputs(B, H, L, D, seed):
 
 
 @pytest.mark.parametrize("variant,L,D,H", [("cog", 17776, 64, 2), ("wan", 32760, 128, 1),
-                                          ("cog", 1000, 64, 3)])
+                                          ("cog", 1000, 64, 3),
+                                          ("wan", 40960, 128, 1)])   # the largest supported: nb = 320
 def test_mask_predict_matches_oracle(variant, L, D, H):
     import vblade
     from vblade.attention import retain_counts
@@ -329,3 +330,12 @@ def test_sample_offsets_match_torch_topk_and_rng_order():
     ref_q = attention.draw_sample_offsets(2, 5, DEV, generator=g2)
     ref_k = attention.draw_sample_offsets(2, 5, DEV, generator=g2)
     assert torch.equal(q_off, ref_q) and torch.equal(k_off, ref_k)
+
+
+def test_mask_predict_rejects_sequences_past_its_block_limit():
+    """nb = 321 sampled blocks exceeds the predictor's LDS row buffers: a loud error, no launch."""
+    L, D = 321 * 128, 64
+    q = torch.zeros(1, 1, L, D, dtype=torch.bfloat16, device=DEV)
+    off = torch.arange(32, dtype=torch.int32, device=DEV).view(1, 1, 32)
+    with pytest.raises(RuntimeError, match="too long"):
+        _ops().mask_predict(q, q, off, off, min_keep=1, max_keep=4)
