@@ -339,3 +339,22 @@ def test_mask_predict_rejects_sequences_past_its_block_limit():
     off = torch.arange(32, dtype=torch.int32, device=DEV).view(1, 1, 32)
     with pytest.raises(RuntimeError, match="too long"):
         _ops().mask_predict(q, q, off, off, min_keep=1, max_keep=4)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_forward_at_its_largest_key_count(D):
+    """Lk = 131072 keys (1024 key blocks, the kernel's list limit). A q-block's output depends only
+    on its mask row, so the oracle checks four q-blocks against their own rows; 1025 blocks raise."""
+    L = 1024 * 128
+    q, k, v = (_rand(1, 1, L, D, seed=80 + s) for s in range(3))
+    mask = O.block_mask_from_density(1, 1, 1024, 1024, 0.01, seed=D)
+    mask[0, 0, :, -1] = True   # the last key block on every row (its DMA ends at the slice's end)
+    out = _ops().attention_fwd(q.to(DEV), k.to(DEV), v.to(DEV), block_mask=mask.to(DEV))
+    out = out.float().cpu()
+    for i in (0, 1, 511, 1023):
+        rows = slice(i * 128, (i + 1) * 128)
+        ref, _ = O.block_sparse_attention(q[:, :, rows], k, v, mask[:, :, i:i + 1])
+        assert (out[:, :, rows] - ref).abs().max() <= _tol(torch.bfloat16)
+    big = torch.zeros(1, 1, L + 128, D, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="too long"):
+        _ops().attention_fwd(big, big, big, block_mask=torch.ones(1, 1, 1025, 1025, dtype=torch.bool, device=DEV))
