@@ -358,3 +358,33 @@ def test_forward_at_its_largest_key_count(D):
     big = torch.zeros(1, 1, L + 128, D, dtype=torch.bfloat16, device=DEV)
     with pytest.raises(RuntimeError, match="too long"):
         _ops().attention_fwd(big, big, big, block_mask=torch.ones(1, 1, 1025, 1025, dtype=torch.bool, device=DEV))
+
+
+def test_reference_signature_varlen_with_an_empty_sequence():
+    """A zero-length sequence between two others (cu_seqlens [0, 300, 300, 855]): its workgroups
+    exit at once and the neighbours' rows match the oracle."""
+    import vblade
+    H, D = 3, 64
+    starts, lens = [0, 300, 300], [300, 0, 555]
+    cu = torch.tensor([0, 300, 300, 855], dtype=torch.int32)
+    q, k, v = (_rand(855, H, D, seed=90 + s) for s in range(3))
+    nb = (max(lens) + 127) // 128
+    base = O.block_mask_from_density(3, 2, nb, nb, 0.4, seed=12)
+    hmt = torch.tensor([1, 0, 1], dtype=torch.int32)
+    out, lse, _ = vblade.block_sparse_attn_func(
+        q.to(DEV), k.to(DEV), v.to(DEV), cu.to(DEV), cu.to(DEV), hmt.to(DEV),
+        torch.zeros(3 * H, dtype=torch.int32, device=DEV), base.to(DEV), max(lens), max(lens), 0.0,
+        deterministic=True, softmax_scale=None, is_causal=False, exact_streaming=False,
+        return_attn_probs=True)
+    for b, (s0, n) in enumerate(zip(starts, lens)):
+        if n == 0:
+            continue
+        qb, kb, vb = (t[s0:s0 + n].transpose(0, 1)[None] for t in (q, k, v))
+        nbb = (n + 127) // 128
+        m = torch.ones(1, H, nbb, nbb, dtype=torch.bool)
+        m[0, 0] = base[b, 0, :nbb, :nbb]
+        m[0, 2] = base[b, 1, :nbb, :nbb]
+        ref, ref_lse = O.block_sparse_attention(qb, kb, vb, m)
+        got = out[s0:s0 + n].transpose(0, 1)[None].float().cpu()
+        assert (got - ref).abs().max() <= 2.5e-2
+        assert (lse[b, :, :n].cpu() - ref_lse[0]).abs().max() <= 2e-3
