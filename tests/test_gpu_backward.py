@@ -10,6 +10,7 @@ errors of ~4e-3 relative.
 import math
 
 import pytest
+import numpy as np
 import torch
 
 import bsa_oracle as O
@@ -89,17 +90,17 @@ def test_bwd_empty_rows_and_columns_and_determinism():
         assert rel(g, r) <= TOL
 
 
-def test_block_sparse_attn_func_autograd_varlen():
+@pytest.mark.parametrize("lens", [[300, 170], [300, 0, 170]])   # the second with an empty sequence
+def test_block_sparse_attn_func_autograd_varlen(lens):
     """Reference-API drop-in (block_sparse_attn_func, varlen layout, head_mask_type = ones ->
     per-head masks) differentiated by torch.autograd, per sequence against the oracle."""
     import vblade
     H, D = 2, 64
-    lens = [300, 170]
     tot = sum(lens)
     q, k, v, do = (_rand(tot, H, D, seed=20 + s) for s in range(4))
-    cu = torch.tensor([0, lens[0], tot], dtype=torch.int32)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), dtype=torch.int32)
     nb = (max(lens) + 127) // 128
-    mask = O.block_mask_from_density(2, H, nb, nb, 0.5, seed=4)
+    mask = O.block_mask_from_density(len(lens), H, nb, nb, 0.5, seed=4)
     qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
     out = vblade.block_sparse_attn_func(qd, kd, vd, cu.to(DEV), cu.to(DEV),
                                         torch.ones(H, dtype=torch.int32, device=DEV), None,
@@ -107,6 +108,8 @@ def test_block_sparse_attn_func_autograd_varlen():
                                         deterministic=True)
     out.backward(do.to(DEV))
     for bi, Lb in enumerate(lens):
+        if Lb == 0:
+            continue
         s0 = int(cu[bi])
         sl = lambda t: t[s0:s0 + Lb].permute(1, 0, 2)[None].float()  # noqa: E731
         nbb = (Lb + 127) // 128
