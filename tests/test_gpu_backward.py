@@ -9,8 +9,8 @@ errors of ~4e-3 relative.
 """
 import math
 
-import pytest
 import numpy as np
+import pytest
 import torch
 
 import bsa_oracle as O
