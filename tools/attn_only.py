@@ -43,10 +43,14 @@ with torch.no_grad():
     ko = vblade.draw_sample_offsets(1, H, dev)
     _, mask = m.predict_mask(q, k, qo, ko)
     kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
+    # the module's K/V source (gather_kv="auto": gathered rows at D=128, Gilbert copies at D=64), so
+    # the counters describe the same kernel variant that bench.py times
+    gather = (D == 128) if m.gather_kv == "auto" else bool(m.gather_kv)
+    k_src, v_src, kv_rows = (k, v, rows) if gather else (k_r, v_r, None)
     for _ in range(n):
         if what in ("attn", "all"):
-            ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp, vp=vp,
-                              kp_log_bias=math.log(m.sample_gap), heavy_rows=m.force_tail)
+            ops.attention_fwd(q, k_src, v_src, block_mask=mask, q_rows=rows, kv_rows=kv_rows, kp=kp,
+                              vp=vp, kp_log_bias=math.log(m.sample_gap), heavy_rows=m.force_tail)
         if what in ("pred", "all"):
             m.predict_mask(q, k, qo, ko)
     torch.cuda.synchronize()
