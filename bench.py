@@ -13,9 +13,20 @@ HBM before the timed region, cycled across calls.
 Attention-only frames/s = frames / (time of 8 x layers calls). The transformer's GEMMs, VAE and
 scheduler are not in the hot path and are not timed.
 
-N GPUs: one process per GPU (torchrun), each rank renders its own videos (prompt-batch replicas,
-no data-path collective) — barrier + synchronize around the timed region, time = max
-over ranks, value = all ranks' frames / time ("scaling": "weak").
+N GPUs: one process per GPU, each rank renders its own videos (prompt-batch replicas, no
+data-path collective). ``--gpus N`` without a launcher's WORLD_SIZE spawns the N
+worker processes itself (one per GPU, as the reference's simple_multiprocess_sampler.py:304-309
+does); under torchrun the launcher's ranks are used. An RCCL barrier + synchronize brackets the
+timed region, the job time is the max over ranks, and ``value`` = frames rendered by ALL ranks /
+that time (whole-job aggregate, "scaling": "weak"); ``per_gpu_frames_per_s`` = value / N.
+
+Rank 0 at N=1 adds (``--no-extras`` skips the sweep and the backward):
+  roofline        attn_fwd_kernel: algorithmic FLOPs / HIP-event launch time, PMC traffic
+  quality         PSNR and max|err| of head 0 of the timed config vs the oracle (same mask)
+  points          Wan at the energy rule, CogVideoX at fixed densities 0.05/0.3/0.5/0.7
+                  (0.05: achieved HBM GB/s vs 8 TB/s), each vs dense SDPA
+  backward        the training path's vb_attn_bwd at the reference operating point
+  cpu_baseline    the reference's CPU SDPA path on BASELINE config 1 (oracle/ref_cpu_path.py)
 """
 from __future__ import annotations
 
@@ -26,6 +37,7 @@ import json
 import math
 import os
 import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -51,7 +63,7 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -62,11 +74,51 @@ def parse():
     ap.add_argument("--sets", type=int, default=3, help="distinct resident q/k/v sets")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the density/Wan points, the backward and the quality check")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes (roofline.traffic = null)")
-    return ap.parse_args()
+    ap.add_argument("--stub-cpu", action="store_true", help=argparse.SUPPRESS)  # launcher tests
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_workers(n: int, argv: list[str]) -> int:
+    """Start ``n`` fresh worker processes of this script, one per GPU, before anything touches a
+    GPU (the parent never does). Each gets RANK/LOCAL_RANK/WORLD_SIZE and a 127.0.0.1
+    rendezvous. Rank 0 prints the JSON line. If a worker fails, the others are stopped so none
+    waits at a barrier. Returns the first non-zero exit code (0 if all succeeded)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for other in live:
+                    other.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 1
+
+
+# ---------------------------------------------------------------------------------- workload
 def realistic_qkv(H, L, D, seed, device):
     g = torch.Generator(device=device).manual_seed(seed)
     cent = torch.randn(1, H, L // 128 + 1, D, generator=g, device=device)
@@ -103,6 +155,12 @@ def attn_flops(mask: torch.Tensor, L: int, D: int, Lkp: int) -> float:
     return 4.0 * D * pairs + 4.0 * heads * L * Lkp * D
 
 
+def attn_alg_bytes(H, L, D, Lkp) -> int:
+    """Compulsory bytes of one fused launch: Q read + O written once, every K/V row
+    read at least once (the kept blocks cover every key block), pooled K/V, the mask."""
+    return H * (4 * L * D * 2) + H * 2 * Lkp * D * 2 + H * ((L + 127) // 128) ** 2
+
+
 def max_over_ranks(elapsed: float, dev) -> float:
     """The job's time = the slowest rank's (weak scaling: every rank renders its own videos).
     Works on any initialised process group (RCCL on the GPU box, gloo in the CPU tests)."""
@@ -121,11 +179,35 @@ def whole_job_frames_per_s(world: int, frames: int, steps: int, elapsed: float) 
     return world * frames * steps / elapsed
 
 
-def main():
-    args = parse()
+def _ranks_seen(world: int, rank: int, dev) -> list[int]:
+    """Every rank reports its RANK through the process group (the launcher check)."""
+    import torch.distributed as dist
+    if world == 1:
+        return [rank]
+    t = torch.zeros(world, dtype=torch.int64, device=dev)
+    t[rank] = rank + 1
+    dist.all_reduce(t)
+    return [int(x) - 1 for x in t.tolist()]
+
+
+# ---------------------------------------------------------------------------------- main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_workers(args.gpus, argv))
+    run(args)
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and "WORLD_SIZE" in os.environ and rank == 0:
+        print(f"bench: --gpus {args.gpus} but the launcher started {world} ranks; using {world}",
+              file=sys.stderr)
+    if args.stub_cpu:
+        return run_stub(args, world, rank)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -178,6 +260,7 @@ def main():
         elapsed = time.perf_counter() - t0
         events, mod.attn_events = mod.attn_events, None
     elapsed = max_over_ranks(elapsed, dev)
+    ranks = _ranks_seen(world, rank, dev)
     ms_per_step = 1000.0 * elapsed / args.steps
     ms_per_call = ms_per_step / calls
     value = whole_job_frames_per_s(world, frames, args.steps, elapsed)
@@ -210,6 +293,10 @@ def main():
                      else f"fixed density {args.density}"),
             "parallelism": f"replicas x{world} (prompt-batch DP, no collective)",
         },
+        "value_is": "whole-job aggregate: frames rendered by all ranks / max-over-ranks time",
+        "per_gpu_frames_per_s": round(value / world, 4),
+        "aggregate_frames_per_s": round(value, 4),
+        "ranks": ranks,
         "ms_per_call": round(ms_per_call, 4),
         "mean_sparsity": round(sparsity, 4),
     }
@@ -230,13 +317,65 @@ def main():
                 result["roofline"]["traffic"] = traffic["bytes"]
                 result["roofline"]["traffic_detail"] = traffic
         result["roofline"]["algorithmic_bytes"] = extra["alg_bytes"]
-        if not args.no_cpu_baseline:
-            result["cpu_baseline"] = (cpu_baseline_ml(calls, frames) if ml
-                                      else cpu_baseline(args.variant, calls, frames))
+        if world == 1 and not args.no_extras and not ml:
+            result["quality"] = quality_vs_oracle(mod, sets[0], args.variant)
+        if world == 1 and not args.no_extras and args.variant == "cog" and args.density is None:
+            dense_cache = {"cog": dense_ms}
+            result["points"] = [measure_point(v, d, dev, dense_cache)
+                                for v, d in (("wan", None), ("cog", 0.05), ("cog", 0.3),
+                                             ("cog", 0.5), ("cog", 0.7))]
+            result["backward"] = measure_backward("cog", dev)
+        if world == 1 and not args.no_cpu_baseline:
+            base = "cog" if args.variant == "cog-ml" else args.variant
+            result["cpu_baseline"] = cpu_baseline_sdpa(base)
+            result["cpu_oracle_port"] = (cpu_baseline_ml(calls, frames) if ml
+                                         else cpu_baseline(args.variant, calls, frames))
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def run_stub(args, world, rank):
+    """The launcher and timing contract with the GPU work replaced by a rank-dependent CPU sleep
+    (gloo): used by tests/test_multi_rank.py to check N workers, distinct ranks and the
+    max-over-ranks time without a GPU."""
+    import torch.distributed as dist
+    dev = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.02 * (rank + 1))
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    ranks = _ranks_seen(world, rank, dev)
+    value = whole_job_frames_per_s(world, 49, args.steps, elapsed)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": value, "n_gpus": world, "ranks": ranks,
+                          "ms_per_step": 1000.0 * elapsed / args.steps,
+                          "per_gpu_frames_per_s": value / world}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------------- measurement
+def dense_sdpa_ms(q, k, v, reps=5):
+    """Dense bf16 SDPA (PyTorch-ROCm) on the same shapes: ms per call, HIP events."""
+    stream = torch.cuda.current_stream(q.device)
+    for _ in range(2):
+        torch.nn.functional.scaled_dot_product_attention(q, k, v)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(reps):
+        torch.nn.functional.scaled_dot_product_attention(q, k, v)
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
 
 
 def measure_kernels(mod, sets, L, H, D, dev, args, events, rng_state, calls):
@@ -280,27 +419,138 @@ def measure_kernels(mod, sets, L, H, D, dev, args, events, rng_state, calls):
             "flops_per_launch": flops,
         }
     }
-    # compulsory bytes of one launch: Q read + O written once, every K/V row read at
-    # least once (the kept blocks cover every key block), pooled K/V, the mask
-    alg_bytes = H * (4 * L * D * 2) + H * 2 * Lkp * D * 2 + H * ((L + 127) // 128) ** 2
+    alg_bytes = attn_alg_bytes(H, L, D, Lkp)
     if ml:   # Q read + O written once, both KV pyramids (15/8 of the padded rows) read once, mask
         R = 15 * ((L + 127) // 128 * 128) // 8
         alg_bytes = H * (2 * L * D * 2) + H * 2 * R * D * 2 + H * ((L + 127) // 128) ** 2
     out = {"top": top, "alg_bytes": alg_bytes}
     if not args.no_dense:
         q, k, v = sets[0]
-        stream = torch.cuda.current_stream(dev)
-        for _ in range(2):
-            torch.nn.functional.scaled_dot_product_attention(q, k, v)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(5):
-            torch.nn.functional.scaled_dot_product_attention(q, k, v)
-        b.record(stream)
-        torch.cuda.synchronize()
-        out["dense_ms"] = a.elapsed_time(b) / 5
+        out["dense_ms"] = dense_sdpa_ms(q, k, v)
     return out
+
+
+def measure_point(variant, density, dev, dense_cache, calls=None, seed=500):
+    """One more operating point, measured in-process on fresh resident inputs: one denoising
+    step's calls (layers) of the whole module, timed with events, the attention launches timed
+    individually, and their FLOPs replayed from the same RNG state (as the main line)."""
+    import vblade
+    V = VARIANTS[variant]
+    H, D, layers, frames = V["H"], V["D"], V["layers"], V["frames"]
+    calls = calls or layers
+    over = {} if density is None else dict(min_retain_ratio=density, max_retain_ratio=density)
+    mod = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **over)
+    L = mod.gilbert_rearranger.seq_len
+    Lkp = (L + mod.sample_gap - 1) // mod.sample_gap
+    sets = [realistic_qkv(H, L, D, seed + s, dev) for s in range(2)]
+    with torch.no_grad():
+        for c in range(4):
+            mod(*sets[c % 2])
+        torch.cuda.synchronize()
+        rng = torch.cuda.get_rng_state(dev)
+        mod.attn_events = []
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for c in range(calls):
+            mod(*sets[c % 2])
+        b.record()
+        torch.cuda.synchronize()
+        ms_call = a.elapsed_time(b) / calls
+        ev, mod.attn_events = mod.attn_events, None
+        attn_ms = sum(x.elapsed_time(y) for x, y in ev) / len(ev)
+        torch.cuda.set_rng_state(rng, dev)
+        flops = 0.0
+        for c in range(calls):
+            q, k, _ = sets[c % 2]
+            _, mask = mod.predict_mask(q, k)
+            flops += attn_flops(mask, L, D, Lkp)
+        flops /= calls
+        if variant not in dense_cache or dense_cache[variant] is None:
+            dense_cache[variant] = dense_sdpa_ms(*sets[0])
+    tfs = flops / (attn_ms * 1e-3) / 1e12
+    alg = attn_alg_bytes(H, L, D, Lkp)
+    res = {
+        "variant": variant, "mask": "energy rule" if density is None else f"density {density}",
+        "mean_sparsity": round(mod.sparsity, 4),
+        "frames_per_s": round(frames / (ms_call * 1e-3 * DENOISE_STEPS * layers), 3),
+        "ms_per_call": round(ms_call, 4),
+        "dense_sdpa_ms_per_call": round(dense_cache[variant], 4),
+        "speedup_vs_dense_sdpa": round(dense_cache[variant] / ms_call, 3),
+        "attn_fwd_ms": round(attn_ms, 4),
+        "attn_fwd_tflops": round(tfs, 2),
+        "mfma_frac": round(tfs / PEAK_BF16_TFLOPS, 4),
+        "algorithmic_bytes": alg,
+        "hbm_gbs_algorithmic": round(alg / (attn_ms * 1e-3) / 1e9, 1),
+        "hbm_frac": round(alg / (attn_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+    }
+    del sets
+    torch.cuda.empty_cache()
+    return res
+
+
+def measure_backward(variant, dev, reps=6):
+    """The training path's backward (vb_attn_bwd: both branches, alpha detached, pooled grads
+    through the mean pool) at the reference operating point, timed with HIP events around each
+    launch; algorithmic FLOPs = 2.5 x the forward's (5 GEMMs per kept block pair against 2)."""
+    import vblade
+    from vblade import ops
+    V = VARIANTS[variant]
+    H, D = V["H"], V["D"]
+    mod = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+    L = mod.gilbert_rearranger.seq_len
+    Lkp = (L + mod.sample_gap - 1) // mod.sample_gap
+    q, k, v = (t.requires_grad_() for t in realistic_qkv(H, L, D, 700, dev))
+    dout = torch.randn(1, H, L, D, device=dev, dtype=torch.bfloat16)
+    events = []
+    orig = ops.attention_bwd
+
+    def timed(*a, **kw):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = orig(*a, **kw)
+        e1.record()
+        events.append((e0, e1))
+        return r
+
+    ops.attention_bwd = timed
+    flops = 0.0
+    try:
+        for i in range(reps + 2):
+            out = mod(q, k, v)
+            if i >= 2:
+                flops += attn_flops(mod.last_mask, L, D, Lkp)
+            out.backward(dout)
+            q.grad = k.grad = v.grad = None
+        torch.cuda.synchronize()
+    finally:
+        ops.attention_bwd = orig
+    ms = sum(a.elapsed_time(b) for a, b in events[2:]) / reps
+    bflops = 2.5 * flops / reps
+    tfs = bflops / (ms * 1e-3) / 1e12
+    return {"variant": variant, "kernel": "vb_attn_bwd (bwd_prep + bwd_dkdv + bwd_dq)",
+            "mask": "energy rule (reference defaults)", "avg_ms": round(ms, 4),
+            "flops_per_call": bflops, "achieved": round(tfs, 2), "unit": "TFLOP/s",
+            "peak": PEAK_BF16_TFLOPS, "frac": round(tfs / PEAK_BF16_TFLOPS, 4),
+            "launches_timed": reps}
+
+
+def quality_vs_oracle(mod, qkv, variant):
+    """Head 0 of one call of the timed configuration against the oracle's reference-faithful
+    adaptive path (two branches + bf16 combine) with the GPU's own mask (SURVEY §8d Quality)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bsa_oracle as O
+    q, k, v = qkv
+    out = mod(q, k, v)
+    mask = mod.last_mask[:, :1].bool().cpu()
+    cfg = O.AdaptiveConfig.cogvideox() if variant == "cog" else O.AdaptiveConfig.wan()
+    ref = O.adaptive_attention(q[:, :1].cpu(), k[:, :1].cpu(), v[:, :1].cpu(), cfg, None, None,
+                               mask=mask, store_dtype=torch.bfloat16)["out"]
+    got = out[:, :1].float().cpu()
+    mse = torch.mean((got.double() - ref.double()) ** 2).item()
+    peak = ref.abs().max().item()
+    return {"head": 0, "psnr_db": round(10 * math.log10(peak * peak / max(mse, 1e-30)), 2),
+            "max_abs": round((got - ref).abs().max().item(), 5),
+            "vs": "oracle/bsa_oracle.adaptive_attention (reference rounding), same mask"}
 
 
 def pmc_traffic(variant, timeout=300):
@@ -341,6 +591,31 @@ def pmc_traffic(variant, timeout=300):
                       "traffic = 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)"}
 
 
+# ---------------------------------------------------------------------------------- CPU baselines
+def cpu_baseline_sdpa(variant):
+    """the reference's CPU attention path (F.scaled_dot_product_attention with the
+    50 % block mask as a token mask; blocksparseattn.py:93-94) on config 1's inputs, 1 warm-up +
+    median of 3, on a head slice scaled to all heads, threads = the host cores this process may
+    use. Baseline only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_cpu_path as R
+    heads = 8 if variant == "cog" else 2
+    r = R.time_cpu_sdpa(variant, heads=heads)
+    c = R.CONFIGS[variant]
+    return {"value": round(r["masked_frames_per_s"], 6), "unit": "frames/s",
+            "cores": r["threads"], "kind": "reference",
+            "cpu_model": r["cpu_model"], "os_cpu_count": r["os_cpu_count"],
+            "masked_s_per_call": round(r["masked_s_per_call"], 3),
+            "dense_s_per_call": round(r["dense_s_per_call"], 3),
+            "dense_frames_per_s": round(r["dense_frames_per_s"], 6),
+            "sample": f"reference CPU path F.scaled_dot_product_attention(q,k,v,attn_mask=token "
+                      f"mask) on BASELINE config 1 inputs [1,{c['H']},{c['L']},{c['D']}] bf16, "
+                      f"50% block mask (seeds 0-3): {heads} of {c['H']} heads timed (1 warm-up + "
+                      f"median of 3), scaled x{c['H'] // heads} heads x {DENOISE_STEPS * c['layers']} "
+                      f"calls per video; threads = cgroup CPU quota of the box "
+                      f"({r['threads']} of os.cpu_count()={r['os_cpu_count']})"}
+
+
 def cpu_baseline_ml(calls, frames):
     """The multi-level oracle (oracle/ml_oracle.py: sampler, pooled scores, level mask, pyramid,
     multi-level softmax) timed on this host's cores: 2 heads of one call, scaled to a video."""
@@ -374,13 +649,14 @@ def cpu_baseline_ml(calls, frames):
 
 def cpu_baseline(variant, calls, frames):
     """The oracle (CPU restatement of the whole adaptive path, oracle/bsa_oracle.py) timed on
-    this host's cores on a bounded sample: a sixth (cog) or a quarter (wan) of the heads of one attention call at the full sequence
-    length, scaled to a whole video's calls. Baseline only."""
+    this host's cores on a bounded sample: a twelfth (cog) or a sixth (wan) of the heads of one
+    attention call at the full sequence length, scaled to a whole video's calls. Reported beside
+    cpu_baseline (the reference's own CPU path) as a second, labelled number."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import bsa_oracle as O
     cfg = O.AdaptiveConfig.cogvideox() if variant == "cog" else O.AdaptiveConfig.wan()
     V = VARIANTS[variant]
-    heads = 8 if variant == "cog" else 3   # about 10 s of CPU work on the GPU box host
+    heads = 4 if variant == "cog" else 2
     L = cfg.width * cfg.height * cfg.depth + cfg.text_length
     g = torch.Generator().manual_seed(0)
     cent = torch.randn(1, heads, L // 128 + 1, V["D"], generator=g).repeat_interleave(128, 2)[:, :, :L]

@@ -89,6 +89,22 @@ def test_empty_row_outputs_zero_and_neg_inf_lse():
     assert (out.float().cpu()[0, 0, :128] - ref[0, 0, :128]).abs().max() <= 2.5e-2
 
 
+def test_reference_signature_empty_row_lse_is_pos_inf():
+    """block_sparse_attn_func (the FlashAttention-2-based op) reports +inf LSE for a query row
+    with no kept key block and a zero output row; the module path keeps -inf (above)."""
+    import vblade
+    q, k, v = (_rand(384, 1, 64, seed=s) for s in range(3))
+    mask = torch.ones(1, 1, 3, 3, dtype=torch.bool)
+    mask[0, 0, 1] = False
+    cu = torch.tensor([0, 384], dtype=torch.int32, device=DEV)
+    out, lse, _ = vblade.block_sparse_attn_func(
+        q.to(DEV), k.to(DEV), v.to(DEV), cu, cu, torch.ones(1, dtype=torch.int32, device=DEV),
+        None, mask.to(DEV), 384, 384, 0.0, deterministic=True, return_attn_probs=True)
+    assert torch.all(out[128:256] == 0)
+    assert torch.all(torch.isposinf(lse[0, 0, 128:256]))
+    assert torch.all(torch.isfinite(lse[0, 0, :128]))
+
+
 def test_online_softmax_rescale_branch_is_exercised():
     """Spike one key late in the key order so the running max jumps (guide §5.4 rule 26)."""
     q, k, v = (_rand(1, 1, 700, 64, seed=20 + s) for s in range(3))

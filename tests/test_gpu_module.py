@@ -241,3 +241,62 @@ def test_full_size_wan_gather_path_is_deterministic():
             outs.append(m(q, k, v))
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("variant", ["cog", "wan"])
+def test_patched_processor_end_to_end_through_hip_module(variant):
+    """a11 on the GPU: the setter patches a fake transformer, the block's processor runs the
+    projections/norm/RoPE around the HIP module, and the result equals the same processor with
+    the oracle's adaptive path (same mask) as inner_attention."""
+    import torch.nn as nn
+    import vblade
+    from test_patch import FakeAttention, _rope_tables
+
+    heads, hd = 2, (64 if variant == "cog" else 128)
+    dim = heads * hd
+    geo = dict(width=12, height=8, depth=6, log_every=0)
+    text = 26 if variant == "cog" else 0
+
+    class Block(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.attn1 = FakeAttention(dim, heads, qk_norm="head" if variant == "cog" else "full")
+
+    model = nn.Module()
+    blocks = nn.ModuleList([Block(), Block()])
+    if variant == "cog":
+        model.transformer_blocks = blocks
+        inner = vblade.set_block_sparse_attn_cogvideox(model, text_length=text, **geo)
+    else:
+        model.blocks = blocks
+        inner = vblade.set_adaptive_block_sparse_attn_wanx(model, **geo)
+    model = model.to(DEV).to(torch.bfloat16)
+    attn = blocks[0].attn1
+    N = 12 * 8 * 6
+    g = torch.Generator().manual_seed(9)
+    hidden = torch.randn(1, N, dim, generator=g).to(DEV, torch.bfloat16)
+    cos_sin, freqs = _rope_tables(N, hd)
+    with torch.no_grad():
+        if variant == "cog":
+            enc = torch.randn(1, text, dim, generator=g).to(DEV, torch.bfloat16)
+            rope = tuple(t.to(DEV) for t in cos_sin)
+            got = attn.processor(attn, hidden, enc, image_rotary_emb=rope)[0]
+        else:
+            got = attn.processor(attn, hidden, None, rotary_emb=freqs.to(DEV))
+        mask = inner.last_mask.bool().cpu()
+        cfg = (O.AdaptiveConfig.cogvideox(width=12, height=8, depth=6, text_length=text)
+               if variant == "cog" else O.AdaptiveConfig.wan(width=12, height=8, depth=6))
+
+        class OracleInner(nn.Module):
+            def forward(self, q, k, v):
+                r = O.adaptive_attention(q.cpu(), k.cpu(), v.cpu(), cfg, None, None, mask=mask,
+                                         store_dtype=torch.bfloat16)["out"]
+                return r.to(q.device, q.dtype)
+
+        for b in blocks:
+            b.attn1.inner_attention = OracleInner()
+        if variant == "cog":
+            ref = attn.processor(attn, hidden, enc, image_rotary_emb=rope)[0]
+        else:
+            ref = attn.processor(attn, hidden, None, rotary_emb=freqs.to(DEV))
+    assert psnr(got.float().cpu(), ref.float().cpu()) >= 40

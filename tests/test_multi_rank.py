@@ -50,3 +50,26 @@ def test_single_process_is_identity():
     import bench
     assert bench.max_over_ranks(1.25, torch.device("cpu")) == 1.25
     assert bench.whole_job_frames_per_s(1, 49, 2, 0.5) == pytest.approx(196.0)
+
+
+def test_bench_self_launches_n_workers():
+    """bench.py --gpus 2 without a launcher's WORLD_SIZE starts 2 fresh worker processes (the
+    GPU work stubbed by a CPU sleep of 20 ms x (rank+1) per step, gloo): rank 0 prints one line
+    that saw 2 distinct ranks and the slower rank's time."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--stub-cpu", "--steps", "5", "--warmup", "0"], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["ranks"] == [0, 1]
+    assert res["ms_per_step"] >= 40.0          # rank 1 sleeps 40 ms per step
+    assert res["value"] == pytest.approx(2 * 49 * 5 / (res["ms_per_step"] * 5 / 1000.0))
+    assert res["per_gpu_frames_per_s"] == pytest.approx(res["value"] / 2)

@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Run only the fused attention kernel (and optionally the predictor) N times on CogVideoX / Wan
 shapes — a target for rocprofv3 counter collection."""
-import math
 import os
 import sys
 
@@ -50,7 +49,7 @@ with torch.no_grad():
     for _ in range(n):
         if what in ("attn", "all"):
             ops.attention_fwd(q, k_src, v_src, block_mask=mask, q_rows=rows, kv_rows=kv_rows, kp=kp,
-                              vp=vp, kp_log_bias=math.log(m.sample_gap), heavy_rows=m.force_tail)
+                              vp=vp, kp_log_bias=m._log_gap(q.dtype), heavy_rows=m.force_tail)
         if what in ("pred", "all"):
             m.predict_mask(q, k, qo, ko)
     torch.cuda.synchronize()

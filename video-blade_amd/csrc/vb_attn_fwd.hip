@@ -920,7 +920,9 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       const float v = (m + __log2f(lt)) * kLn2;
       float* dst = p.lse + b * p.lse_s[0] + h * p.lse_s[1] + (p.cu_q ? qg : qrow);
       if (nan_head) *reinterpret_cast<uint32_t*>(dst) = 0x7FC00000u;
-      else *dst = v;
+      // a row with no kept key: -inf on the module path; +inf on the reference-signature entry
+      // (cu_q set), FlashAttention-2's convention for an empty softmax (normalize_softmax_lse)
+      else *dst = (p.cu_q && !(lt > 0.f)) ? INFINITY : v;
     }
   }
 }

@@ -20,7 +20,6 @@ cogvideo_blocksparseattn.py:45-46 so the RNG stream matches the reference) stays
 """
 from __future__ import annotations
 
-import math
 from typing import Optional
 
 import numpy as np
@@ -192,6 +191,12 @@ class AdaptiveBlockSparseAttn(nn.Module):
             self._fold_slots()
         return getattr(self, "_folded", 0.0) / self.sparsity_counter
 
+    def _log_gap(self, dtype) -> float:
+        """ln(gap) as the reference computes it: torch.log of a tensor in the LSE's storage
+        dtype (lse is cast to q.dtype at :324, the log taken in it at :375-376), i.e. 2.703125
+        for g=15 in bf16. The training path's combine rounds it the same way (vb_pool.hip)."""
+        return float(torch.log(torch.tensor(float(self.sample_gap), dtype=dtype)).item())
+
     # -------------------------------------------------------------------------------- forward
     def predict_mask(self, q, k, q_off=None, k_off=None, count=None, staged_event=None, pool=None):
         """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores. ``pool``
@@ -218,6 +223,11 @@ class AdaptiveBlockSparseAttn(nn.Module):
                 q_off: Optional[torch.Tensor] = None, k_off: Optional[torch.Tensor] = None,
                 block_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, H, L, D = q.shape
+        if k.shape != q.shape or v.shape != q.shape:
+            # the reference's index_select over the Gilbert index fails on a shorter k/v (e.g. the
+            # Wan I2V image keys); every launch below assumes q's [B,H,L,D] for k and v
+            raise ValueError(f"k and v must have q's shape {tuple(q.shape)}, got "
+                             f"{tuple(k.shape)} and {tuple(v.shape)}")
         if self.use_rearrange and L != self.gilbert_rearranger.seq_len:
             raise ValueError(f"sequence length {L} != {self.gilbert_rearranger.seq_len} expected "
                              f"by the Gilbert grid (width/height/depth/text_length)")
@@ -268,7 +278,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
             out = ops.attention_fwd(q, k_src, v_src, block_mask=mask, q_rows=rows, kv_rows=kv_rows,
-                                    kp=kp, vp=vp, kp_log_bias=math.log(self.sample_gap),
+                                    kp=kp, vp=vp, kp_log_bias=self._log_gap(q.dtype),
                                     heavy_rows=self.force_tail)
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)

@@ -30,11 +30,10 @@ class _BlockSparseAttnFunc(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, _dlse):
-        from . import backward as bw
         q, k, v, out, lse, cu_q, cu_k, hmt, mask = ctx.saved_tensors
         max_q, max_k, scale = ctx.meta
-        dq, dk, dv = bw.block_sparse_attn_bwd(dout, q, k, v, out, lse, cu_q, cu_k, hmt, mask,
-                                              max_q, max_k, scale)
+        dq, dk, dv = ops.block_sparse_attn_bwd(dout, q, k, v, out, lse, cu_q, cu_k, hmt, None,
+                                               mask, max_q, max_k, softmax_scale=scale)
         return (dq, dk, dv) + (None,) * 12
 
 
@@ -67,10 +66,12 @@ class _AdaptiveSplitFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        from . import backward as bw
         q, k_r, v_r, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp = ctx.saved_tensors
-        dq, dk, dv = bw.adaptive_split_bwd(dout.contiguous(), q, k_r, v_r, mask, rows, out1, lse1,
-                                           out2, lse2, alpha, kp, vp, ctx.gap, heavy_rows=2)
+        # per-branch FA2 backward with dO1 = alpha*dO, dO2 = (1-alpha)*dO; pooled-branch K/V grads
+        # through the mean pool and the Gilbert gather, returned in the caller's row order
+        dq, dk, dv = ops.attention_bwd(dout.contiguous(), q, k_r, v_r, out1, lse1, block_mask=mask,
+                                       q_rows=rows, kv_rows=rows, kp=kp, vp=vp, out2=out2,
+                                       lse2=lse2, alpha=alpha, gap=ctx.gap, heavy_rows=2)
         return dq, dk, dv, None, None, None
 
 

@@ -294,6 +294,9 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     ``pool=(v, gap, outs)``: the pooled K/V pass (vb_pool_kv of k, v through ``rows``) run by extra
     workgroups of the score kernel's launch on the current stream; ``outs`` = pool_kv_outputs(k,
     gap, reordered) receives kp, vp[, k_r, v_r]."""
+    if k.shape != q.shape:
+        raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
+                         f"got k {tuple(k.shape)}")
     dev = _require_gpu(q, k, q_off, k_off, rows)
     q, k = _aligned_bhld(q), _aligned_bhld(k)
     B, H, L, D = q.shape
@@ -328,8 +331,11 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     if pool is not None:
         v, gap, outs = pool
         v = _aligned_bhld(v)
-        if v.shape != k.shape or outs[0].shape != (B, H, (L + int(gap) - 1) // int(gap), D):
-            raise ValueError("mask_predict: pool v must match k and outs come from pool_kv_outputs")
+        if v.shape != k.shape:
+            raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
+                             f"got v {tuple(v.shape)}")
+        if outs[0].shape != (B, H, (L + int(gap) - 1) // int(gap), D):
+            raise ValueError("mask_predict: pool outputs must come from pool_kv_outputs(k, gap)")
         a.pool_v, a.pool_v_stride, a.pool_gap = v.data_ptr(), _s3(v), int(gap)
         a.pool_kp, a.pool_vp = outs[0].data_ptr(), outs[1].data_ptr()
         if len(outs) > 2:
@@ -386,6 +392,11 @@ def pool_kv(k, v, gap: int, rows=None, reordered: bool = False, stream=None, out
     same pass. ``stream`` (a torch.cuda.Stream) launches there instead of the current stream; the
     outputs are still allocated on the current stream, which must wait for ``stream`` before
     using them."""
+    if v.shape != k.shape:
+        raise ValueError(f"pool_kv: k and v must have the same shape, got {tuple(k.shape)} and "
+                         f"{tuple(v.shape)}")
+    if rows is not None and rows.numel() != k.shape[2]:
+        raise ValueError(f"pool_kv: rows has {rows.numel()} entries for {k.shape[2]} keys")
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
     if stream is not None:   # read (and written) on the side stream: no reuse before it is done
@@ -445,6 +456,11 @@ def kv_pyramid(k, v, rows=None, stream=None, out=None):
     """vb_kv_pyramid: K/V [B,H,L,D] (reordered through `rows`) -> pyramids [B,H,15*Lpad/8,D]:
     level-1 rows (zero beyond L), then the 2x, 4x, 8x mean-pooled rows (replicate padding).
     ``stream``: as pool_kv."""
+    if v.shape != k.shape:
+        raise ValueError(f"pool_kv: k and v must have the same shape, got {tuple(k.shape)} and "
+                         f"{tuple(v.shape)}")
+    if rows is not None and rows.numel() != k.shape[2]:
+        raise ValueError(f"pool_kv: rows has {rows.numel()} entries for {k.shape[2]} keys")
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
     if stream is not None:   # see pool_kv
