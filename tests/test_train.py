@@ -153,3 +153,72 @@ def test_qk_dump_counter_and_layout_match_the_reference(tmp_path):
         c = t * 3 + l
         assert torch.equal(d["q"], qs[c]) and torch.equal(d["k"], qs[c] + 0.5)
     assert m.counter == 14
+
+
+def _tdm_batches(n_micro, per, L=32, hidden=64, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n_micro):
+        out.append((torch.randn(per, L, hidden, generator=g), torch.randn(per, L, hidden, generator=g),
+                    torch.rand(per, 1, 1, generator=g) + 0.5))
+    return out
+
+
+def _tdm_models(seed=0):
+    student = _model(seed=seed)
+    _perturb_b(student)
+    teacher = _model(seed=seed)            # the base model: LoRA B = 0
+    return student, teacher
+
+
+def test_tdm_step_updates_both_models_and_fake_starts_as_student():
+    student, teacher = _tdm_models()
+    step = T.TDMTrainStep(student, teacher, lr=1e-2, lr_fake=1e-2, accum=2)
+    assert all(torch.equal(a, b) for a, b in zip(step.fake.lora_parameters(), student.lora_parameters()))
+    assert step.fake.transformer_blocks[0].inner_attention is not student.transformer_blocks[0].inner_attention
+    g0 = [p.detach().clone() for p in student.lora_parameters()]
+    f0 = [p.detach().clone() for p in step.fake.lora_parameters()]
+    t0 = [p.detach().clone() for p in teacher.parameters()]
+    lf, lg = step(_tdm_batches(2, 2))
+    assert torch.isfinite(lf) and torch.isfinite(lg)
+    assert any(not torch.equal(a, b) for a, b in zip(g0, student.lora_parameters()))
+    assert any(not torch.equal(a, b) for a, b in zip(f0, step.fake.lora_parameters()))
+    assert all(torch.equal(a, b) for a, b in zip(t0, teacher.parameters()))      # frozen
+    assert step.opt_g.defaults["betas"] == (0.0, 0.95) and step.opt_d.defaults["betas"] == (0.0, 0.95)
+
+
+def _tdm_dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    student, teacher = _tdm_models()
+    step = T.TDMTrainStep(student, teacher, lr=1e-2, lr_fake=1e-2, accum=2, bucket_bytes=4096)
+    full = _tdm_batches(2, 4)
+    mine = [tuple(t[2 * rank:2 * rank + 2] for t in mb) for mb in full]   # this rank's half
+    step(mine)
+    q.put((rank, [p.detach().numpy().copy() for p in student.lora_parameters()],
+           [p.detach().numpy().copy() for p in step.fake.lora_parameters()]))
+    step.close()
+    dist.destroy_process_group()
+
+
+def test_tdm_two_rank_all_reduce_of_both_models_equals_single_process():
+    """Two ranks on half micro-batches end with the student AND the fake model equal to one
+    process on the whole micro-batches (each model's own bucketed all-reduce)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tdm_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (g, f) for r, g, f in (q.get(timeout=180) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    student, teacher = _tdm_models()
+    step = T.TDMTrainStep(student, teacher, lr=1e-2, lr_fake=1e-2, accum=2, distributed=False)
+    step(_tdm_batches(2, 4))
+    for which, mine in ((0, student.lora_parameters()), (1, step.fake.lora_parameters())):
+        for a, b, c in zip(res[0][which], res[1][which], mine):
+            a, b = torch.from_numpy(a), torch.from_numpy(b)
+            assert torch.equal(a, b)
+            assert torch.allclose(a, c.detach(), atol=5e-6, rtol=1e-4)

@@ -44,7 +44,7 @@ def main():
     dev = torch.device("cuda")
     for variant in (["cog", "wan"] if a.variant == "both" else [a.variant]):
         H, D = (48, 64) if variant == "cog" else (12, 128)
-        m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+        m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **({"gather_kv": os.environ["AB_GATHER"] == "1"} if "AB_GATHER" in os.environ else {}))
         L = m.gilbert_rearranger.seq_len
         q, k, v = realistic_qkv(H, L, D, 0, dev)
         rows = m._rows(dev)

@@ -21,7 +21,7 @@ for variant in ("cog", "wan"):
     q, k, v = realistic_qkv(H, L, D, 0, dev)
     qo = vblade.draw_sample_offsets(1, H, dev)
     ko = vblade.draw_sample_offsets(1, H, dev)
-    for dbg in ("0", "1", "2", "3", "5"):
+    for dbg in (sys.argv[2].split(",") if len(sys.argv) > 2 else ("0", "1", "2", "3", "5")):
         os.environ["VB_DEBUG_PRED"] = dbg
         for _ in range(3):
             m.predict_mask(q, k, qo, ko)

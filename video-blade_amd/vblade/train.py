@@ -254,6 +254,104 @@ class TrainStep:
         return total
 
 
+class TDMTrainStep:
+    """The TDM joint step with its two trained models (train_cogvideo_tdm.py:1301-1325, loop
+    :1640-1737): a student (the K-step generator) and a fake-score model initialised as a deep copy
+    of it (:1301), each with its own AdamW (betas (0, 0.95): ``args.adam_beta1 = 0`` at :1310),
+    learning rate, gradient clipping and data-parallel gradient exchange (two accelerators,
+    :1318-1325), plus a frozen teacher ("real" model). Every micro-batch runs, in the reference's
+    order:
+
+    1. fake-score update (:1640-1688): the student's prediction without grad, the fake model's
+       prediction WITH grad (sparse attention under autograd), the weighted regression loss
+       ``mean(w * (fake - student)^2)``, backward into the fake model;
+    2. generator update (:1690-1737): the student's prediction WITH grad, teacher and fake
+       predictions without grad, the revised target ``student + real - fake`` (detached), the
+       pseudo-Huber loss over ``weighting_factor`` (:1719-1727), backward into the student.
+
+    On the last micro-batch of an accumulation window each model's reducer exchanges its LoRA
+    gradients (one bucketed all-reduce per model), then clip + AdamW per model. The diffusion
+    specifics (noise schedules, timesteps, K-step ODE states) are outside the hot path: a
+    micro-batch gives the student's input ``x_gen`` (the noisy ODE state), the re-noised input the
+    fake and teacher models see ``x_noisy`` (noisy_model_latents) and the regression weight ``w``
+    (1 / (1 - alphas_cumprod[t])). The three models share nothing; each
+    carries its own sparse-attention module (a deep copy, as at :1301)."""
+
+    def __init__(self, student: StandInTransformer, teacher: Optional[StandInTransformer] = None, *,
+                 lr: float = 1e-4, lr_fake: float = 1e-4, betas=(0.0, 0.95), weight_decay: float = 1e-4,
+                 eps: float = 1e-8, max_grad_norm: float = 1.0, accum: int = 1, group=None,
+                 bucket_bytes: int = 64 << 20, huber_c: float = 1e-3, distributed: Optional[bool] = None):
+        import copy
+        self.student = student
+        self.fake = copy.deepcopy(student)
+        self.teacher = teacher if teacher is not None else copy.deepcopy(student)
+        for q in self.teacher.parameters():
+            q.requires_grad_(False)
+        self.accum = accum
+        self.max_grad_norm = max_grad_norm
+        self.huber_c = huber_c
+        self.g_params = student.lora_parameters()
+        self.f_params = self.fake.lora_parameters()
+
+        def adamw(params, lr_):
+            return torch.optim.AdamW(params, lr=lr_, betas=betas, eps=eps, weight_decay=weight_decay,
+                                     foreach=all(q.is_cuda for q in params))
+
+        self.opt_g = adamw(self.g_params, lr)
+        self.opt_d = adamw(self.f_params, lr_fake)
+        if distributed is None:
+            distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.red_g = BucketedGradReducer(self.g_params, group, bucket_bytes) if distributed else None
+        self.red_d = BucketedGradReducer(self.f_params, group, bucket_bytes) if distributed else None
+
+    def _step(self, params, opt, red):
+        if red is not None:
+            red.finish()
+        gnorm = torch.nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return gnorm
+
+    def __call__(self, micro_batches: List[tuple]):
+        """micro_batches: ``accum`` tuples (x_gen, x_noisy, w). Returns (loss_fake, loss_gen)."""
+        assert len(micro_batches) == self.accum
+        lf, lg = [], []
+        for i, (x_gen, x_noisy, w) in enumerate(micro_batches):
+            last = i == self.accum - 1
+            # 1. fake-score update
+            if self.red_d is not None:
+                self.red_d.enable(last)
+            with torch.no_grad():
+                target = self.student(x_gen)
+            fake = self.fake(x_noisy)
+            loss_f = (w * (fake.float() - target.float()) ** 2).mean() / self.accum
+            loss_f.backward()
+            lf.append(loss_f.detach())
+            if last:
+                self.last_grad_norm_fake = self._step(self.f_params, self.opt_d, self.red_d)
+            # 2. generator update
+            if self.red_g is not None:
+                self.red_g.enable(last)
+            pred = self.student(x_gen)
+            with torch.no_grad():
+                real = self.teacher(x_noisy)
+                fake_g = self.fake(x_noisy)
+                revised = (pred.detach() + real - fake_g).float()
+                weighting = (pred.detach().float() - real.float()).abs().mean(
+                    dim=tuple(range(1, pred.dim())), keepdim=True).clamp(max=5.0)
+            loss_g = pseudo_huber(pred, revised, self.huber_c, weighting) / self.accum
+            loss_g.backward()
+            lg.append(loss_g.detach())
+            if last:
+                self.last_grad_norm = self._step(self.g_params, self.opt_g, self.red_g)
+        return torch.stack(lf).sum(), torch.stack(lg).sum()
+
+    def close(self):
+        for r in (self.red_g, self.red_d):
+            if r is not None:
+                r.close()
+
+
 # ------------------------------------------------------------------------------------------------
 # LoRA checkpoint (diffusers save_lora_weights format)
 # ------------------------------------------------------------------------------------------------
