@@ -57,7 +57,10 @@ int vb_gilbert3d_perm(int width, int height, int depth, int32_t* perm_out);
  *                 replace_ones_with_count); m<0 (streaming) -> that head's output is NaN.
  *   streaming_info ignored (only used by streaming heads)
  *   base_blockmask uint8/bool [batch, n_sparse, ceil(max_q/128), ceil(max_k/128)] contiguous
- *   out_unpad     [total_q, H, D]; softmax_lse fp32 [batch, H, max_seqlen_q] (natural log)
+ *   out_unpad     [total_q, H, D]; softmax_lse fp32 [batch, H, max_seqlen_q] (natural log).
+ *                 A query row with no kept key block gets a zero output row and lse = +inf,
+ *                 FlashAttention-2's convention for an empty softmax (its normalize_softmax_lse);
+ *                 the native entry vb_attn_fwd reports -inf for such rows instead.
  *   p_dropout must be 0, is_causal/exact_streaming must be 0 (the reference's call) else
  *   VB_ERR_UNSUPPORTED. softmax_scale <= 0 means head_dim^-1/2. `deterministic` is accepted
  *   and ignored (the forward is deterministic).

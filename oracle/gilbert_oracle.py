@@ -2,7 +2,7 @@
 
 Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
 this module, and only as the checker. The product computes the permutation in C++
-(``video-blade_amd/csrc/vb_gilbert.cpp``, exported as ``vb_gilbert3d_perm``).
+(``video-blade_amd/csrc/vb_host.cpp``, exported as ``vb_gilbert3d_perm``).
 
 Follows the generalized-Hilbert ("gilbert") curve of J. Cervený (BSD-2, 2018) as used by the
 reference at ``cogvideox/train/special_attentions_local/utils/gilbert3d.py:6-167`` and the index

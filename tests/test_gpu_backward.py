@@ -181,19 +181,48 @@ def test_full_size_adaptive_backward_one_head(variant, D):
     _check_adaptive_grads(m, cfg, q, k, v, do)
 
 
-def test_training_batch_b2_matches_per_sample():
-    """B=2 (training batches are B=5 in the reference): each sample's grads equal the B=1 grads."""
+@pytest.mark.parametrize("B", [2, 5])
+def test_training_batch_matches_per_sample(B):
+    """B=5 is the reference's TDM micro-batch (train_tdm_1.sh:14): each sample's grads equal the
+    B=1 grads."""
     m, cfg = _small_module("cog")
     L = m.gilbert_rearranger.seq_len
-    q, k, v, do = _realistic(2, 2, L, 64, seed=8)
+    q, k, v, do = _realistic(B, 2, L, 64, seed=8)
     qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
     out = m(qd, kd, vd)
     out.backward(do.to(DEV))
     mask_model = m.last_mask
-    for b in range(2):
+    for b in range(B):
         qb, kb, vb = (t[b:b + 1].to(DEV).requires_grad_(True) for t in (q, k, v))
         ob = m(qb, kb, vb, block_mask=mask_model[b:b + 1])
         ob.backward(do[b:b + 1].to(DEV))
         assert math.isclose(rel(qb.grad, qd.grad[b:b + 1].cpu()), 0.0, abs_tol=1e-6)
         assert math.isclose(rel(kb.grad, kd.grad[b:b + 1].cpu()), 0.0, abs_tol=1e-6)
         assert math.isclose(rel(vb.grad, vd.grad[b:b + 1].cpu()), 0.0, abs_tol=1e-6)
+
+
+def test_full_size_b5_training_batch_one_head():
+    """BASELINE config 5's micro-batch at the full CogVideoX sequence: q,k,v [5,1,17776,64] with
+    grad. Every sample's dq/dk/dv equals its own B=1 run, and sample 0 matches the oracle's
+    reference-semantics backward."""
+    import vblade
+    m = vblade.AdaptiveBlockSparseAttn("cog", log_every=0)
+    cfg = O.AdaptiveConfig.cogvideox()
+    L = m.gilbert_rearranger.seq_len
+    q, k, v, do = _realistic(5, 1, L, 64, seed=11)
+    qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+    out = m(qd, kd, vd)
+    out.backward(do.to(DEV))
+    mask = m.last_mask
+    for b in range(5):
+        qb, kb, vb = (t[b:b + 1].to(DEV).requires_grad_(True) for t in (q, k, v))
+        ob = m(qb, kb, vb, block_mask=mask[b:b + 1])
+        ob.backward(do[b:b + 1].to(DEV))
+        assert torch.equal(ob, out[b:b + 1])
+        for g1, g5 in ((qb.grad, qd.grad), (kb.grad, kd.grad), (vb.grad, vd.grad)):
+            assert torch.equal(g1, g5[b:b + 1])
+    fwd = O.adaptive_attention(q[:1], k[:1], v[:1], cfg, None, None, mask=mask[:1].bool().cpu())
+    assert rel(out[:1].detach().float().cpu(), fwd["out"]) <= TOL
+    rq, rk, rv = O.adaptive_attention_bwd(q[:1], k[:1], v[:1], do[:1], cfg, fwd)
+    for name, g, r in (("dq", qd.grad[:1], rq), ("dk", kd.grad[:1], rk), ("dv", vd.grad[:1], rv)):
+        assert rel(g, r) <= TOL, (name, rel(g, r))
