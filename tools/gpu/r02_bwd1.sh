@@ -1,0 +1,12 @@
+#!/bin/bash
+# backward v1 (dK/dV heavy-first order, -Delta seeded dP, descriptor-DMA dQ): parity, then A/B vs b0
+set -o pipefail
+OUT=gpurun_out/r02_bwd1
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_backward.py tests/test_gpu_multilevel.py tests/test_gpu_train.py -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python tools/ab.py b0 b1 b0 b1 --what bwd --rounds 6 > $OUT/ab.txt 2>&1
+rc=$?; echo "ab rc=$rc"; grep -v amdgpu.ids $OUT/ab.txt
+exit $rc

@@ -89,11 +89,13 @@ if __name__ == "__main__":
     ap.add_argument("--variant", default="both")
     ap.add_argument("--densities", default="")
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--only-bwd", action="store_true", help="skip the forward timings (PMC passes)")
     a = ap.parse_args()
     with torch.no_grad():
         for var in (["cog", "wan"] if a.variant == "both" else [a.variant]):
-            run(var)
+            if not a.only_bwd:
+                run(var)
             for d in [float(x) for x in a.densities.split(",") if x]:
                 run(var, d)
-            if a.bwd:
+            if a.bwd or a.only_bwd:
                 run_bwd(var)

@@ -200,10 +200,30 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
   const int nkb = kPooled ? p.nbkp : p.nbk;
   // pooled-key blocks see every q-block: their work is split into psplit q-block ranges (split
   // innermost, so a key block's workgroups run together); main blocks XCD-contiguous
+  // Main blocks: the `heavy_rows` last key blocks of every head (CogVideoX's forced dense text
+  // columns, kept by every q-block: ~8x the average column's tiles) go first over all XCDs, then
+  // each XCD takes a contiguous head-major range with key blocks in descending order. Ascending
+  // order put every head's two heavy columns at the end of its range, so the last head of each
+  // XCD's range left a long tail (measured: 1.26 waves per SIMD on average at 2 possible).
   const int split = kPooled ? (int)blockIdx.x % p.psplit : 0;
-  const int lin = kPooled ? (int)blockIdx.x / p.psplit : xcd_linear(blockIdx.x, nkb * BH);
-  const int bh = lin / nkb;
-  const int kblk = lin % nkb;
+  int bh, kblk;
+  if (kPooled) {
+    const int lin = (int)blockIdx.x / p.psplit;
+    bh = lin / nkb;
+    kblk = lin % nkb;
+  } else {
+    const int hr = kML ? 0 : min(p.heavy_rows, nkb);
+    const int n_heavy = hr * BH;
+    if ((int)blockIdx.x < n_heavy) {
+      kblk = nkb - 1 - (int)(blockIdx.x / BH);
+      bh = blockIdx.x % BH;
+    } else {
+      const int cols_left = nkb - hr;
+      const int lin = xcd_linear(blockIdx.x - n_heavy, cols_left * BH);
+      bh = lin / cols_left;
+      kblk = cols_left - 1 - lin % cols_left;
+    }
+  }
   const int b = bh / p.H, h = bh % p.H;
 
   int Lq = p.Lq, Lk = p.Lk;
@@ -377,9 +397,18 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
     if (kML && kPooled) act = (list_bits[t >> 1] >> my_blk_bit) & 1;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      // dP's accumulator starts at -Delta of its row (register r = row 4j+e of this u half), so
+      // dS = P * (dO.V^T - Delta) needs no subtraction per score
       f32x16 s, dp;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 Dv = *reinterpret_cast<const f32x4*>(st + (fL + 1) * 64 + 32 * u + 8 * j + 4 * half);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[4 * j + e] = 0.f;
+          dp[4 * j + e] = -Dv[e];
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         s = T::mfma32(lds_b128<T>(qt, dual_off<D>(32 * u + l32, 2 * ks + half)), kf[ks], s);
@@ -389,7 +418,6 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 Lv = *reinterpret_cast<const f32x4*>(st + fL * 64 + 32 * u + 8 * j + 4 * half);
-        const f32x4 Dv = *reinterpret_cast<const f32x4*>(st + (fL + 1) * 64 + 32 * u + 8 * j + 4 * half);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * j + e;
@@ -397,7 +425,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
           if (kML) pr = act ? exp2_fast(fmaf(s[r], p.c, lvl_bias - Lv[e])) : 0.f;
           else pr = exp2_fast(fmaf(s[r], p.c, -Lv[e]));
           s[r] = pr;
-          dp[r] = pr * (dp[r] - Dv[e]);
+          dp[r] = pr * dp[r];
         }
       }
       // dV^T += dO^T.P and dK^T += Q^T.dS over (16-row half sb, 32-wide d tile dt) steps; the four
@@ -577,8 +605,11 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 // ------------------------------------------------------------------------------------------------
 // dQ: one workgroup per (b, h, 128-row q-block); kept full-resolution tiles then pooled tiles
 // ------------------------------------------------------------------------------------------------
+#ifndef VB_DQ_WAVES_D64
+#define VB_DQ_WAVES_D64 2   // waves per SIMD the D=64 dQ kernel is register-budgeted for
+#endif
 template <int D, class T, bool kPool, bool kML = false>
-__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64) bwd_dq_kernel(const BwdParams p) {
   using namespace bwd;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
@@ -754,28 +785,63 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
       klen = min(kT, p.Lkp - kstart);
     }
   };
-  auto issue = [&](int t) __attribute__((always_inline)) {
-    int kstart = 0, klen = kT;
-    int qsrc[4] = {0, 0, 0, 0};
-    if (kML) {
+  // Tile t -> ring slot by LDS-DMA through buffer descriptors (as the dK/dV kernel): this wave
+  // issues instructions i = wave + 4k (K tile first, then V). A lane's part of each instruction
+  // (row within the tile, swizzled chunk) is a fixed 32-bit voffset per key source; the tile's first
+  // key is the scalar soffset, so no per-lane 64-bit address math runs per tile. The host checks
+  // that every (b,h) slice spans < 2 GiB.
+  static_assert(kInst % 4 == 0, "every wave issues the same number of DMA instructions");
+  constexpr int kPer = kInst / 4;
+  const int krowb = 2 * (int)p.ks[2], vrowb = 2 * (int)p.vs[2];
+  const int kprowb = kPool ? 2 * (int)p.kps[2] : 0, vprowb = kPool ? 2 * (int)p.vps[2] : 0;
+  const int src_rows = kML ? 15 * (p.Lpad / 8) : Lk;
+  const srd_t k_srd = make_srd(use_main ? kbase : nullptr, use_main ? (int)((int64_t)(src_rows - 1) * krowb + RB) : 0);
+  const srd_t v_srd = make_srd(use_main ? vbase : nullptr, use_main ? (int)((int64_t)(src_rows - 1) * vrowb + RB) : 0);
+  const srd_t kp_srd = make_srd(kPool ? kpbase : nullptr, kPool ? (int)((int64_t)(p.Lkp - 1) * kprowb + RB) : 0);
+  const srd_t vp_srd = make_srd(kPool ? vpbase : nullptr, kPool ? (int)((int64_t)(p.Lkp - 1) * vprowb + RB) : 0);
+  int dr[kPer], dc16[kPer], voff_m[kPer], voff_p[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = wave + 4 * k;
+    const bool isv = k >= kPer / 2;   // i >= kInstTile exactly when k >= kPer / 2
+    const int ii = isv ? i - kInstTile : i;
+    dr[k] = ii * kRowsPerInst + lane / kCh;
+    dc16[k] = 16 * ((lane % kCh) ^ dual_swz<D>(dr[k]));
+    const int rr = kML ? (dr[k] & 15) : dr[k];   // multi-level: row within the 16-row quarter
+    voff_m[k] = rr * (isv ? vrowb : krowb) + dc16[k];
+    voff_p[k] = dr[k] * (isv ? vprowb : kprowb) + dc16[k];
+  }
+  auto issue = [&](int t, auto SLOT) __attribute__((always_inline)) {
+    constexpr int slot = decltype(SLOT)::value;
+    uint8_t* buf = smem + slot * kBufBytes;
+    if constexpr (kML) {
+      int qsrc[4];
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd) qsrc[qd] = __builtin_amdgcn_readfirstlane(ml_quarter(t, qd));
-    } else {
-      tile_keys(t, kstart, klen);
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const bool isv = k >= kPer / 2;
+        const int i = wave + 4 * k;
+        const int ii = isv ? i - kInstTile : i;
+        const int qd = (ii * kRowsPerInst) >> 4;   // wave-uniform: kRowsPerInst divides 16
+        const int q = qd == 0 ? qsrc[0] : qd == 1 ? qsrc[1] : qd == 2 ? qsrc[2] : qsrc[3];
+        dma16(isv ? v_srd : k_srd, buf + i * 1024, voff_m[k],
+              __builtin_amdgcn_readfirstlane(q * (isv ? vrowb : krowb)));
+      }
+      return;
     }
+    int kstart, klen;
+    tile_keys(t, kstart, klen);
     const bool pooled = kPool && t >= ntm;
-    uint8_t* buf = smem + (kRing == 2 ? (t & 1) : t % kRing) * kBufBytes;
-    for (int i = wave; i < kInst; i += 4) {
-      const bool isv = i >= kInstTile;
-      const int ii = isv ? i - kInstTile : i;
-      const int r = ii * kRowsPerInst + lane / kCh;
-      const int c = (lane % kCh) ^ dual_swz<D>(r);
-      const int64_t key = kML ? qsrc[r >> 4] + (r & 15) : kstart + min(r, klen - 1);
-      const uint8_t* src;
-      if (pooled) src = isv ? vpbase + key * 2 * p.vps[2] : kpbase + key * 2 * p.kps[2];
-      else src = isv ? vbase + key * 2 * p.vs[2] : kbase + key * 2 * p.ks[2];
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 16),
-                                       (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const bool isv = k >= kPer / 2;
+      const int i = wave + 4 * k;
+      const int rowb = pooled ? (isv ? vprowb : kprowb) : (isv ? vrowb : krowb);
+      const srd_t sd = pooled ? (isv ? vp_srd : kp_srd) : (isv ? v_srd : k_srd);
+      int voff = pooled ? voff_p[k] : voff_m[k];
+      if (klen < kT) voff = min(dr[k], klen - 1) * rowb + dc16[k];   // tail: replicate the last key
+      dma16(sd, buf + i * 1024, voff, __builtin_amdgcn_readfirstlane(kstart * rowb));
     }
   };
 
@@ -788,10 +854,14 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
   constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
   const bool many = wave < (kInst & 3);
 
-  if (ntiles > 0) issue(0);
-  if (kRing == 3 && ntiles > 1) issue(1);
-  for (int t = 0; t < ntiles; ++t) {
-    if (kRing == 2 && t + 1 < ntiles) issue(t + 1);
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if (ntiles > 0) issue(0, I0{});
+  if (kRing == 3 && ntiles > 1) issue(1, I1{});
+  // The body is instantiated once per ring slot, so every LDS address is an immediate offset.
+  auto body = [&](int t, auto U) __attribute__((always_inline)) {
+    constexpr int u_slot = decltype(U)::value;
+    if (kRing == 2 && t + 1 < ntiles) issue(t + 1, std::integral_constant<int, (u_slot + 1) % kRing>{});
     // retire this wave's part of tile t (tile t+1's stays in flight), then the barrier
     if (t + 1 < ntiles) {
       if (many) VB_WAIT_VMCNT(kHi);
@@ -800,7 +870,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
       VB_WAIT_VMCNT(0);
     }
     __builtin_amdgcn_s_barrier();
-    if (kRing == 3 && t + 2 < ntiles) issue(t + 2);
+    if (kRing == 3 && t + 2 < ntiles) issue(t + 2, std::integral_constant<int, (u_slot + 2) % kRing>{});
     int kstart, klen;
     float nL;
     bool pooled;
@@ -814,13 +884,18 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
       nL = -(pooled ? L2 : L1);
     }
     const float Dr = pooled ? D2 : D1;
-    const uint8_t* kt_ = smem + (kRing == 2 ? (t & 1) : t % kRing) * kBufBytes;
+    const uint8_t* kt_ = smem + u_slot * kBufBytes;
     const uint8_t* vt_ = kt_ + kTileBytes;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {   // 32-key halves: S^T, dP^T -> dS^T -> dQ^T
+      // dP^T's accumulator starts at -Delta of the lane's row: dS = P * (dO.V^T - Delta) with no
+      // subtraction per score
       f32x16 s, dp;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        s[r] = 0.f;
+        dp[r] = -Dr;
+      }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         s = T::mfma32(lds_b128<T>(kt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), qf[ks], s);
@@ -833,13 +908,13 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
         for (int r = 0; r < 16; ++r) {
           const bool ok = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half < klen;
           const float pr = ok ? exp2_fast(fmaf(s[r], p.c, nL)) : 0.f;
-          dp[r] = pr * (dp[r] - Dr);
+          dp[r] = pr * dp[r];
         }
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float pr = exp2_fast(fmaf(s[r], p.c, nL));
-          dp[r] = pr * (dp[r] - Dr);
+          dp[r] = pr * dp[r];
         }
       }
       // dQ^T += K^T.dS^T over (16-key half sb, d tile dt) steps, reads one step ahead (lgkmcnt(2))
@@ -868,6 +943,12 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dq_kernel
       }
     }
     if (kRing == 2) __builtin_amdgcn_s_barrier();   // slot t % 2 is refilled by the next issue
+  };
+  for (int t0 = 0; t0 < ntiles; t0 += kRing) {
+    body(t0, I0{});
+    if (t0 + 1 < ntiles) body(t0 + 1, I1{});
+    if constexpr (kRing > 2)
+      if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
   }
 
   if (!qvalid) return;
@@ -1033,6 +1114,9 @@ extern "C" int vb_attn_bwd(const vb_attn_bwd_args* a, void* stream) {
     return fail(VB_ERR_INVALID, "vb_attn_bwd: workspace missing or smaller than vb_attn_bwd_workspace_size()");
   if (!a->q_rows && (!slice_ok(a->Lq, a->q_stride[2], a->D) || !slice_ok(a->Lq, a->dout_stride[2], a->D)))
     return fail(VB_ERR_UNSUPPORTED, "vb_attn_bwd: a q/dout (b,h) slice spans >= 2 GiB");
+  if (!slice_ok(a->Lk, a->k_stride[2], a->D) || !slice_ok(a->Lk, a->v_stride[2], a->D) ||
+      (pool && (!slice_ok(a->Lkp, a->kp_stride[2], a->D) || !slice_ok(a->Lkp, a->vp_stride[2], a->D))))
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_bwd: a k/v/kp/vp (b,h) slice spans >= 2 GiB");
   uint8_t* ws = reinterpret_cast<uint8_t*>(a->workspace);
 
   PrepParams pp{};
@@ -1119,6 +1203,8 @@ extern "C" int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, c
     return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: workspace missing or too small");
   if (!slice_ok(max_seqlen_q, (int64_t)num_heads * head_dim, head_dim))
     return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: a sequence's q/dout span >= 2 GiB");
+  if (!slice_ok(max_seqlen_k, (int64_t)num_heads * head_dim, head_dim))
+    return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: a sequence's k/v span >= 2 GiB");
   const void* ptrs[] = {dout, q_unpad, k_unpad, v_unpad, out_unpad, dq, dk, dv};
   for (const void* q : ptrs)
     if (!al16(q)) return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: tensors must be 16-byte aligned");
@@ -1214,6 +1300,8 @@ extern "C" int vb_ml_attn_bwd(const vb_ml_attn_bwd_args* a, void* stream) {
     return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: workspace missing or smaller than vb_ml_attn_bwd_workspace_size()");
   if (!a->rows && (!slice_ok(a->L, a->q_stride[2], a->D) || !slice_ok(a->L, a->dout_stride[2], a->D)))
     return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_bwd: a q/dout (b,h) slice spans >= 2 GiB");
+  if ((int64_t)vb_kv_pyramid_rows(a->L) * 2 * a->D >= (int64_t(1) << 31))
+    return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_bwd: a pyramid (b,h) slice spans >= 2 GiB");
   uint8_t* ws = reinterpret_cast<uint8_t*>(a->workspace);
   const int Lpad = nb * 128;
   const int R = 15 * (Lpad / 8);
