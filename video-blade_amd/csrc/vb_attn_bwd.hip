@@ -13,7 +13,8 @@
 // so dO itself is used unscaled and Delta = rowsum(dO * O_branch) (FA2's D_i) per branch.
 //
 // Kernels (all 256 threads = 4 waves, v_mfma_f32_32x32x16, operand maps in vb_tiles.hpp):
-//   bwd_prep_kernel   per row: Delta1/2, L'1/2 -> stats [B*H][ntile64][4][64] fp32; optional
+//   bwd_prep_kernel   per row: -Delta1/2, L'1/2 -> stats [B*H][ntile64][4][64] fp32 (Delta negated:
+//                     it seeds the dP accumulators, see below); optional
 //                     reordered contiguous copies of q and dO (one gather pass instead of one per
 //                     key block that reads them)
 //   bwd_dkdv_kernel   one workgroup per (b, h, 128-key block); wave = 32 keys held in registers;
@@ -51,7 +52,7 @@ struct PrepParams {
   const float* lse; const float* lse2; const float* alpha;  // [B,H,Lq] at the caller's row
   const int32_t* q_rows; const int32_t* cu_q;
   void* q_r; void* do_r;  // [B,H,Lq,D] contiguous reordered copies (written when q_rows != NULL)
-  float* stats;           // [B*H][ntile][4][64]: L'1, Delta1, L'2, Delta2
+  float* stats;           // [B*H][ntile][4][64]: L'1, -Delta1, L'2, -Delta2
   int B, H, Lq, D, ntile;
 };
 
@@ -165,16 +166,22 @@ __global__ void __launch_bounds__(256) bwd_prep_kernel(const PrepParams p) {
   }
   float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
   st[0] = l1;
-  st[64] = d1;
+  st[64] = -d1;
   st[128] = l2;
-  st[192] = d2;
+  st[192] = -d2;
 }
 
 // ------------------------------------------------------------------------------------------------
 // dK / dV: one workgroup per (b, h, 128-key block)
 // ------------------------------------------------------------------------------------------------
+#ifndef VB_BWD_SEED128
+#define VB_BWD_SEED128 0    // D=128: dP seeded with -Delta too (measured 6 % slower on Wan's dK/dV)
+#endif
+#ifndef VB_DKDV_WAVES_D64
+#define VB_DKDV_WAVES_D64 2   // waves per SIMD the D=64 dK/dV kernel is register-budgeted for
+#endif
 template <int D, class T, bool kPooled, bool kML = false>
-__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D64) bwd_dkdv_kernel(const BwdParams p) {
   using namespace bwd;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
@@ -373,6 +380,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 
   const int trr = tr_row(lane), trc = tr_col(lane);
   constexpr int fL = (kPooled && !kML) ? 2 : 0;  // stats fields of this branch
+  constexpr bool kSeed = D == 64 || VB_BWD_SEED128;
 
   if (ntiles > 0) issue(0, 0);
   if (ntiles > 1) issue(1, 1);
@@ -397,8 +405,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
     if (kML && kPooled) act = (list_bits[t >> 1] >> my_blk_bit) & 1;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      // dP's accumulator starts at -Delta of its row (register r = row 4j+e of this u half), so
-      // dS = P * (dO.V^T - Delta) needs no subtraction per score
+      // dP's accumulator starts at -Delta of its row (register r = row 4j+e of this u half; the
+      // stats hold -Delta, read straight into the accumulator), so dS = P * (dO.V^T - Delta) needs
+      // no subtraction per score
       f32x16 s, dp;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -406,7 +415,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           s[4 * j + e] = 0.f;
-          dp[4 * j + e] = -Dv[e];
+          dp[4 * j + e] = kSeed ? Dv[e] : 0.f;
         }
       }
 #pragma unroll
@@ -418,6 +427,8 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 Lv = *reinterpret_cast<const f32x4*>(st + fL * 64 + 32 * u + 8 * j + 4 * half);
+        f32x4 Dv2 = {0.f, 0.f, 0.f, 0.f};
+        if (!kSeed) Dv2 = *reinterpret_cast<const f32x4*>(st + (fL + 1) * 64 + 32 * u + 8 * j + 4 * half);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * j + e;
@@ -425,7 +436,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : 2) bwd_dkdv_kern
           if (kML) pr = act ? exp2_fast(fmaf(s[r], p.c, lvl_bias - Lv[e])) : 0.f;
           else pr = exp2_fast(fmaf(s[r], p.c, -Lv[e]));
           s[r] = pr;
-          dp[r] = pr * dp[r];
+          dp[r] = pr * (kSeed ? dp[r] : dp[r] + Dv2[e]);
         }
       }
       // dV^T += dO^T.P and dK^T += Q^T.dS over (16-row half sb, 32-wide d tile dt) steps; the four
@@ -730,7 +741,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
     }
   }
   const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
-  float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];
+  float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];   // D1, D2 = -Delta
   asm volatile("" : "+v"(L1), "+v"(D1), "+v"(L2), "+v"(D2));
   __syncthreads();
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
@@ -890,11 +901,12 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
     for (int kt = 0; kt < 2; ++kt) {   // 32-key halves: S^T, dP^T -> dS^T -> dQ^T
       // dP^T's accumulator starts at -Delta of the lane's row: dS = P * (dO.V^T - Delta) with no
       // subtraction per score
+      constexpr bool kSeedQ = D == 64 || VB_BWD_SEED128;
       f32x16 s, dp;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         s[r] = 0.f;
-        dp[r] = -Dr;
+        dp[r] = kSeedQ ? Dr : 0.f;
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -908,13 +920,13 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
         for (int r = 0; r < 16; ++r) {
           const bool ok = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half < klen;
           const float pr = ok ? exp2_fast(fmaf(s[r], p.c, nL)) : 0.f;
-          dp[r] = pr * dp[r];
+          dp[r] = pr * (kSeedQ ? dp[r] : dp[r] + Dr);
         }
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float pr = exp2_fast(fmaf(s[r], p.c, nL));
-          dp[r] = pr * dp[r];
+          dp[r] = pr * (kSeedQ ? dp[r] : dp[r] + Dr);
         }
       }
       // dQ^T += K^T.dS^T over (16-key half sb, d tile dt) steps, reads one step ahead (lgkmcnt(2))
