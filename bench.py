@@ -91,17 +91,18 @@ def _free_port() -> int:
     return port
 
 
-def launch_workers(n: int, argv: list[str]) -> int:
-    """Start ``n`` fresh worker processes of this script, one per GPU, before anything touches a
-    GPU (the parent never does). Each gets RANK/LOCAL_RANK/WORLD_SIZE and a 127.0.0.1
-    rendezvous. Rank 0 prints the JSON line. If a worker fails, the others are stopped so none
-    waits at a barrier. Returns the first non-zero exit code (0 if all succeeded)."""
+def launch_workers(n: int, argv: list[str], script: str | None = None) -> int:
+    """Start ``n`` fresh worker processes of ``script`` (default: this file), one per GPU, before
+    anything touches a GPU (the parent never does). Each gets RANK/LOCAL_RANK/WORLD_SIZE and a
+    127.0.0.1 rendezvous. Rank 0 prints the JSON line. If a worker fails, the others are stopped
+    so none waits at a barrier. Returns the first non-zero exit code (0 if all succeeded)."""
     port = _free_port()
     procs = []
+    script = os.path.abspath(script or __file__)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+        procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
     rc = 0
     live = list(procs)
     while live:

@@ -73,3 +73,24 @@ def test_bench_self_launches_n_workers():
     assert res["ms_per_step"] >= 40.0          # rank 1 sleeps 40 ms per step
     assert res["value"] == pytest.approx(2 * 49 * 5 / (res["ms_per_step"] * 5 / 1000.0))
     assert res["per_gpu_frames_per_s"] == pytest.approx(res["value"] / 2)
+
+
+def test_train_bench_self_launches_n_workers():
+    """tools/train_bench.py --gpus 2 starts 2 worker processes itself (the training step stubbed
+    by a CPU sleep of 20 ms x (rank+1), gloo): one line, 2 ranks, the slower rank's time."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "train_bench.py"), "--gpus", "2",
+                        "--stub-cpu", "--steps", "5", "--batch", "5", "--accum", "4"], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["ranks"] == [0, 1]
+    assert res["ms_per_step"] >= 40.0
+    assert res["value"] == pytest.approx(2 * 5 * 4 * 5 / (res["ms_per_step"] * 5 / 1000.0))

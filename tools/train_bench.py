@@ -5,6 +5,7 @@ sparse attention under autograd + gradient checkpointing, with the bucketed RCCL
 all-reduce across ranks (torchrun: one process per GPU).
 
     python tools/train_bench.py [--layers 4] [--batch 1] [--accum 1] [--steps 3] [--warmup 1]
+    python tools/train_bench.py --gpus N ...   (starts N worker processes itself, one per GPU)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/train_bench.py ...
 
 Prints one JSON line: samples/s over all ranks, ms per optimizer step, and the share of the
@@ -68,10 +69,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rank-lora", type=int, default=64)
     ap.add_argument("--variant", default="cog", choices=["cog", "wan"])
-    args = ap.parse_args()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--stub-cpu", action="store_true", help=argparse.SUPPRESS)  # launcher tests
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    import bench
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one fresh process per GPU, as bench.py --gpus N (reference: simple_multiprocess_sampler.py:304-309)
+        sys.exit(bench.launch_workers(args.gpus, argv, script=os.path.abspath(__file__)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub_cpu:
+        return run_stub(args, world, rank)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -109,7 +119,6 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    import bench
     elapsed = bench.max_over_ranks(elapsed, dev)
     if rank == 0:
         ev = timed.events
@@ -138,6 +147,31 @@ def main():
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def run_stub(args, world, rank):
+    """Launcher test path (no GPU): gloo ranks, each step a CPU sleep of 20 ms x (rank + 1) in
+    place of the training step; the same barrier + max-over-ranks timing and JSON line."""
+    import bench
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    ranks = bench._ranks_seen(world, rank, dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.02 * (rank + 1))
+    if world > 1:
+        dist.barrier()
+    elapsed = bench.max_over_ranks(time.perf_counter() - t0, dev)
+    if rank == 0:
+        samples = world * args.batch * args.accum * args.steps
+        print(json.dumps({"metric": "stub", "value": samples / elapsed, "n_gpus": world, "ranks": ranks,
+                          "ms_per_step": 1000.0 * elapsed / args.steps}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
