@@ -743,6 +743,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
   const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
   float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];   // D1, D2 = -Delta
   asm volatile("" : "+v"(L1), "+v"(D1), "+v"(L2), "+v"(D2));
+
   __syncthreads();
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
   int ntm = 2 * nkept;
@@ -865,6 +866,11 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
   constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
   const bool many = wave < (kInst & 3);
 
+  constexpr bool kSeedQ = D == 64 || VB_BWD_SEED128;
+  f32x16 cD, zero;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) cD[r] = zero[r] = 0.f;
+  int cur_cls = -1;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   if (ntiles > 0) issue(0, I0{});
@@ -885,34 +891,41 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
     int kstart, klen;
     float nL;
     bool pooled;
+    int cls;   // tile class (wave-uniform): main/pooled, or the multi-level level
     if (kML) {
       klen = ml_klen(t);
       pooled = false;
-      nL = (float)ml_lvl(t) - L1;   // + log2(level): the +ln p logit bias in the exp2 domain
+      cls = ml_lvl(t);
+      nL = (float)cls - L1;   // + log2(level): the +ln p logit bias in the exp2 domain
     } else {
       tile_keys(t, kstart, klen);
       pooled = kPool && t >= ntm;
+      cls = pooled;
       nL = -(pooled ? L2 : L1);
     }
     const float Dr = pooled ? D2 : D1;
+    if (cls != cur_cls) {   // only where the key source changes: refresh the persistent seeds
+      asm volatile("");
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        cD[r] = kSeedQ ? Dr : 0.f;
+      }
+      cur_cls = cls;
+    }
     const uint8_t* kt_ = smem + u_slot * kBufBytes;
     const uint8_t* vt_ = kt_ + kTileBytes;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {   // 32-key halves: S^T, dP^T -> dS^T -> dQ^T
-      // dP^T's accumulator starts at -Delta of the lane's row: dS = P * (dO.V^T - Delta) with no
-      // subtraction per score
-      constexpr bool kSeedQ = D == 64 || VB_BWD_SEED128;
+      // dP^T's chain starts from cD = -Delta of the lane's row (dS = P * (dO.V^T - Delta) with no
+      // subtraction per score); the seeds are persistent registers read as the MFMA's C operand
       f32x16 s, dp;
+      s = T::mfma32(lds_b128<T>(kt_, dual_off<D>(kt * 32 + l32, half)), qf[0], zero);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s[r] = 0.f;
-        dp[r] = kSeedQ ? Dr : 0.f;
-      }
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+      for (int ks = 1; ks < KS; ++ks)
         s = T::mfma32(lds_b128<T>(kt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), qf[ks], s);
+      dp = T::mfma32(lds_b128<T>(vt_, dual_off<D>(kt * 32 + l32, half)), df[0], cD);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+      for (int ks = 1; ks < KS; ++ks)
         dp = T::mfma32(lds_b128<T>(vt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), df[ks], dp);
       if (klen < kT) {
         asm volatile("");
@@ -1044,11 +1057,14 @@ struct WsLayout {
   uint64_t stats, q_r, do_r, dkp, dvp, dkp_part, dvp_part, total;
   int psplit;
 };
-// pooled-key q-range split: aim at ~3k workgroups for the pooled dK/dV pass
+// pooled-key q-range split: aim at ~3k workgroups per sample for the pooled dK/dV pass. The split
+// sets the order of the partial sums, so it does not depend on B: a sample's gradients are the
+// same bits in any batch (the B=5 training-batch test).
 static int pool_split(int B, int H, int Lq, int Lkp) {
+  (void)B;
   if (Lkp <= 0) return 1;
   const int nbkp = (Lkp + 127) / 128, nbq = (Lq + 127) / 128;
-  const int wg = nbkp * B * H;
+  const int wg = nbkp * H;
   int s = (3072 + wg / 2) / wg;
   return s < 1 ? 1 : (s > nbq ? nbq : s);
 }
