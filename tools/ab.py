@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)
 import vblade  # noqa: E402
 from vblade import _lib, ops  # noqa: E402
-from bench import attn_flops, realistic_qkv  # noqa: E402
+from bench import attn_flops, ml_attn_flops, realistic_qkv  # noqa: E402
 
 
 def load(tag):
@@ -72,6 +72,14 @@ def main():
                                            kv_rows=rows, kp=kp, vp=vp, out2=out2, lse2=lse2,
                                            alpha=alpha, gap=gap, heavy_rows=m.force_tail)[0]
             fl = 2.5 * fl
+        elif a.what == "mlbwd":   # the multi-level path's backward (vb_ml_attn_bwd), dk compared
+            from vblade import multilevel
+            do = torch.randn_like(q)
+            _, lmask = multilevel.predict_level_mask(q, k, rows=rows)
+            kpy, vpy = ops.kv_pyramid(k, v, rows)
+            mo, mlse = ops.ml_attention_fwd(q, kpy, vpy, lmask, q_rows=rows, want_lse=True, heavy_rows=2)
+            fn = lambda: ops.ml_attention_bwd(do, q, kpy, vpy, lmask, mo, mlse, rows=rows)[1]  # noqa
+            fl = 2.5 * ml_attn_flops(lmask, L, D)
         else:
             fn = lambda: m(q, k, v)  # noqa
         ref = None
@@ -86,7 +94,7 @@ def main():
                         ref = out[1].clone()
                     else:
                         print(f"  {t}: mask identical to {a.tags[0]}: {torch.equal(out[1], ref)}")
-                if a.what in ("attn", "bwd"):
+                if a.what in ("attn", "bwd", "mlbwd"):
                     if ref is None:
                         ref = out.float()
                     else:
@@ -105,7 +113,7 @@ def main():
         base = statistics.median(times[keys[0]])
         for kk, t in zip(keys, a.tags):
             md = statistics.median(times[kk])
-            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what in ("attn", "bwd") else ""
+            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what in ("attn", "bwd", "mlbwd") else ""
             print(f"{variant} {a.what} {kk}: median {md:.4f} ms (min {min(times[kk]):.4f}){extra}  "
                   f"x{base / md:.3f} vs {a.tags[0]}", flush=True)
 

@@ -402,7 +402,15 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
     const float* st = reinterpret_cast<const float*>(qt + 2 * kTileBytes);
     // multi-level pooled items: keys of blocks without level 2^e for this q-block take no part
     bool act = true;
-    if (kML && kPooled) act = (list_bits[t >> 1] >> my_blk_bit) & 1;
+    if (kML && kPooled) {
+      act = (list_bits[t >> 1] >> my_blk_bit) & 1;
+      // The item's q-block list is the union over its 2^e key blocks; a wave whose own key
+      // blocks are not at level 2^e for this q-block has nothing to add (P = 0 for all its keys)
+      // and skips the tile's MFMAs, leaving its SIMD to the co-resident waves. A wave holds one
+      // block's keys at levels 2 and 4, two blocks' at level 8. Its tile would add exact zeros,
+      // so the sums are unchanged.
+      if (!__any(act)) return;
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       // dP's accumulator starts at -Delta of its row (register r = row 4j+e of this u half; the
