@@ -96,10 +96,4 @@ struct MlTileSrc {
   int lvl;          // log2 of the level: the logit bias in the exp2 domain
 };
 
-#ifndef VB_FWD_PP
-#define VB_FWD_PP 0   // D=64 inference launches use the 8-wave ping-pong kernel (vb_attn_fwd_pp.hip)
-#endif
-// vb_attn_fwd_pp.hip: launches the ping-pong kernel when it covers the call, else returns -1
-int launch_fwd_pp(const FwdParams& p, int dtype, bool pool, hipStream_t stream);
-
 }  // namespace vb
