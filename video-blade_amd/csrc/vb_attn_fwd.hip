@@ -384,6 +384,10 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   };
   auto issue = [&](const TileSrc src, int slot, int t = 0) __attribute__((always_inline)) {
     uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
+    // this wave's i-th 1 KiB piece of the tile
+    auto piece = [&](int i, srd_t sd, int voff, int soff) __attribute__((always_inline)) {
+      dma16(sd, dst + i * 1024, voff, soff);
+    };
     const bool pooled = kPool && src.pooled;
     if (kKvRows && !pooled) {
       typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -399,7 +403,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       for (int i = 0; i < kInstPerWave; ++i) {
         int voff;   // row * stride + chunk: rows < 2^24 and strides < 2^24 bytes (host-checked)
         asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(voff) : "v"(o[i]), "s"(my_rowb), "v"(my_chunk[i] * 16));
-        dma16(my_rsrc, dst + i * 1024, voff, 0);
+        piece(i, my_rsrc, voff, 0);
       }
       return;
     }
@@ -409,13 +413,12 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       const int vb0 = my_row0 * rowb;
 #pragma unroll
       for (int i = 0; i < kInstPerWave; ++i)
-        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, vb0 + my_rc[i],
-              __builtin_amdgcn_readfirstlane(soff + i * kRowsPerInst * rowb));
+        piece(i, pooled ? my_prsrc : my_rsrc, vb0 + my_rc[i], __builtin_amdgcn_readfirstlane(soff + i * kRowsPerInst * rowb));
     } else {   // tail tile: clamp rows to the last valid key (replicated rows are masked later)
 #pragma unroll
       for (int i = 0; i < kInstPerWave; ++i) {
         const int r = min(my_row0 + i * kRowsPerInst, src.klen - 1);
-        dma16(pooled ? my_prsrc : my_rsrc, dst + i * 1024, r * rowb + my_rc[i], soff);
+        piece(i, pooled ? my_prsrc : my_rsrc, r * rowb + my_rc[i], soff);
       }
     }
   };
@@ -432,7 +435,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   f32x16 cb;
 #pragma unroll
   for (int r = 0; r < 16; ++r) cb[r] = 0.f;
-  float cur_bias = 0.f;
+  int cur_bias_bits = 0;   // bit pattern of the bias folded into cb (0.0f)
   bool first = true;
 #if VB_MFMA_ROWSUM
   // Row sums on the matrix core (D=64 is VALU-bound): lsum += ones . P^T, every register of the
@@ -470,12 +473,15 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     const uint8_t* kl = smem + kSlot * kBufBytes;
     f32x16 s[2];
     if constexpr (kCBias) {
-      if (bias != cur_bias) {   // wave-uniform; only where the tile source changes (pooled, levels)
+      // wave-uniform; only where the tile source changes (pooled, levels). Compared as bit patterns
+      // in SGPRs (a scalar compare; a float compare would run on the VALU every tile)
+      const int bias_bits = __builtin_amdgcn_readfirstlane(__float_as_int(bias));
+      if (bias_bits != cur_bias_bits) {
         asm volatile("");
-        const float db = bias - cur_bias;
+        const float db = bias - __int_as_float(cur_bias_bits);
 #pragma unroll
         for (int r = 0; r < 16; ++r) cb[r] += db;
-        cur_bias = bias;
+        cur_bias_bits = bias_bits;
       }
     }
     // V^T fragments (ds_read_b64_tr_b16) for the first VPRE k-steps, issued before the softmax
