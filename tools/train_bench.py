@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--rank-lora", type=int, default=64)
     ap.add_argument("--variant", default="cog", choices=["cog", "wan"])
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--tdm", action="store_true",
+                    help="the two-model TDM step (student + fake-score model + frozen teacher, two AdamW, "
+                         "two reducers; train_cogvideo_tdm.py:1301-1325, 1640-1737)")
     ap.add_argument("--stub-cpu", action="store_true", help=argparse.SUPPRESS)  # launcher tests
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
@@ -97,11 +100,17 @@ def main():
     L = attn.gilbert_rearranger.seq_len
     model = T.StandInTransformer(args.layers, hidden, heads, args.rank_lora, float(args.rank_lora), timed,
                                  gradient_checkpointing=True, device=dev, seed=0)
-    reducer = T.BucketedGradReducer(model.lora_parameters()) if world > 1 else None
-    step = T.TrainStep(model, lr=1e-4, accum=args.accum, reducer=reducer)
     g = torch.Generator(device=dev).manual_seed(100 + rank)
-    micro = [(torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16(),
-              torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16()) for _ in range(args.accum)]
+    if args.tdm:
+        step = T.TDMTrainStep(model, lr=1e-4, lr_fake=1e-4, accum=args.accum, distributed=world > 1)
+        micro = [(torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16(),
+                  torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16(),
+                  torch.rand(args.batch, 1, 1, generator=g, device=dev) + 0.5) for _ in range(args.accum)]
+    else:
+        reducer = T.BucketedGradReducer(model.lora_parameters()) if world > 1 else None
+        step = T.TrainStep(model, lr=1e-4, accum=args.accum, reducer=reducer)
+        micro = [(torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16(),
+                  torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16()) for _ in range(args.accum)]
     torch.manual_seed(1234 + rank)
     for _ in range(args.warmup):
         step(micro)
@@ -131,7 +140,8 @@ def main():
         ms_step = 1000.0 * elapsed / args.steps
         samples = world * args.batch * args.accum * args.steps
         print(json.dumps({
-            "metric": "TDM-style LoRA training step, stand-in blocks with " +
+            "metric": ("TDM two-model step (student + fake-score + teacher)" if args.tdm else
+                       "TDM-style LoRA training step") + ", stand-in blocks with " +
                       ("CogVideoX-5B" if args.variant == "cog" else "Wan2.1-1.3B") + " attention geometry",
             "value": round(samples / elapsed, 4), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 2),
@@ -143,7 +153,8 @@ def main():
             "attention_fwd_ms_per_step": round(fwd_ms / args.steps, 2),
             "attention_bwd_ms_per_step": round(bwd_ms / args.steps, 2),
             "attention_share": round((fwd_ms + bwd_ms) / args.steps / ms_step, 3),
-            "last_loss": float(loss)}), flush=True)
+            "attention_timed": "student model's calls only (fake/teacher copies untimed)" if args.tdm else "all calls",
+            "last_loss": [float(x) for x in loss] if isinstance(loss, tuple) else float(loss)}), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
