@@ -96,10 +96,4 @@ struct MlTileSrc {
   int lvl;          // log2 of the level: the logit bias in the exp2 domain
 };
 
-#ifndef VB_FWD_SWP
-#define VB_FWD_SWP 0   // D=64 inference launches on Gilbert copies: the software-pipelined kernel
-#endif
-// vb_attn_fwd_swp.hip: launches the software-pipelined kernel when it covers the call, else -1
-int launch_fwd_swp(const FwdParams& p, int dtype, bool pool, hipStream_t stream);
-
 }  // namespace vb
