@@ -23,7 +23,8 @@ that time (whole-job aggregate, "scaling": "weak"); ``per_gpu_frames_per_s`` = v
 Rank 0 at N=1 adds (``--no-extras`` skips the sweep and the backward):
   roofline        attn_fwd_kernel: algorithmic FLOPs / HIP-event launch time, PMC traffic
   quality         PSNR and max|err| of head 0 of the timed config vs the oracle (same mask)
-  points          Wan at the energy rule, CogVideoX at fixed densities 0.05/0.3/0.5/0.7
+  points          Wan at the energy rule, the multi-level sampler op (cog-ml), CogVideoX at fixed
+                  densities 0.05/0.3/0.5/0.7
                   (0.05: achieved HBM GB/s vs 8 TB/s), each vs dense SDPA
   backward        the training path's vb_attn_bwd at the reference operating point
   cpu_baseline    the reference's CPU SDPA path on BASELINE config 1 (oracle/ref_cpu_path.py)
@@ -323,8 +324,8 @@ def run(args):
         if world == 1 and not args.no_extras and args.variant == "cog" and args.density is None:
             dense_cache = {"cog": dense_ms}
             result["points"] = [measure_point(v, d, dev, dense_cache)
-                                for v, d in (("wan", None), ("cog", 0.05), ("cog", 0.3),
-                                             ("cog", 0.5), ("cog", 0.7))]
+                                for v, d in (("wan", None), ("cog-ml", None), ("cog", 0.05),
+                                             ("cog", 0.3), ("cog", 0.5), ("cog", 0.7))]
             result["backward"] = measure_backward("cog", dev)
         if world == 1 and not args.no_cpu_baseline:
             base = "cog" if args.variant == "cog-ml" else args.variant
@@ -439,10 +440,15 @@ def measure_point(variant, density, dev, dense_cache, calls=None, seed=500):
     V = VARIANTS[variant]
     H, D, layers, frames = V["H"], V["D"], V["layers"], V["frames"]
     calls = calls or layers
-    over = {} if density is None else dict(min_retain_ratio=density, max_retain_ratio=density)
-    mod = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **over)
+    ml = variant == "cog-ml"
+    if ml:   # the VBench sampler's multi-level op (cogvideox/sample_evaluate/modify_cogvideo.py:9)
+        from vblade import multilevel
+        mod = multilevel.AdaptiveBlockSparseAttnTrain(log_every=0)
+    else:
+        over = {} if density is None else dict(min_retain_ratio=density, max_retain_ratio=density)
+        mod = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **over)
     L = mod.gilbert_rearranger.seq_len
-    Lkp = (L + mod.sample_gap - 1) // mod.sample_gap
+    Lkp = 0 if ml else (L + mod.sample_gap - 1) // mod.sample_gap
     sets = [realistic_qkv(H, L, D, seed + s, dev) for s in range(2)]
     with torch.no_grad():
         for c in range(4):
@@ -463,20 +469,34 @@ def measure_point(variant, density, dev, dense_cache, calls=None, seed=500):
         flops = 0.0
         for c in range(calls):
             q, k, _ = sets[c % 2]
-            _, mask = mod.predict_mask(q, k)
-            flops += attn_flops(mask, L, D, Lkp)
+            if ml:
+                _, mask = multilevel.predict_level_mask(q, k, rows=mod._rows(q.device),
+                                                        mask_ratios=mod.mask_ratios)
+                flops += ml_attn_flops(mask, L, D)
+            else:
+                _, mask = mod.predict_mask(q, k)
+                flops += attn_flops(mask, L, D, Lkp)
         flops /= calls
-        if variant not in dense_cache or dense_cache[variant] is None:
-            dense_cache[variant] = dense_sdpa_ms(*sets[0])
+        dkey = "cog" if ml else variant
+        if dkey not in dense_cache or dense_cache[dkey] is None:
+            dense_cache[dkey] = dense_sdpa_ms(*sets[0])
+        dense_ms = dense_cache[dkey]
     tfs = flops / (attn_ms * 1e-3) / 1e12
-    alg = attn_alg_bytes(H, L, D, Lkp)
+    if ml:   # Q read + O written once, both KV pyramids (15/8 of the padded rows) read once, mask
+        R = 15 * ((L + 127) // 128 * 128) // 8
+        alg = H * (2 * L * D * 2) + H * 2 * R * D * 2 + H * ((L + 127) // 128) ** 2
+    else:
+        alg = attn_alg_bytes(H, L, D, Lkp)
+    sparsity = mod.sparsity_acc / mod.sparsity_counter if ml else mod.sparsity
     res = {
-        "variant": variant, "mask": "energy rule" if density is None else f"density {density}",
-        "mean_sparsity": round(mod.sparsity, 4),
+        "variant": variant,
+        "mask": ("rank-band level mask (reference mask_ratios)" if ml
+                 else "energy rule" if density is None else f"density {density}"),
+        "mean_sparsity": round(sparsity, 4),
         "frames_per_s": round(frames / (ms_call * 1e-3 * DENOISE_STEPS * layers), 3),
         "ms_per_call": round(ms_call, 4),
-        "dense_sdpa_ms_per_call": round(dense_cache[variant], 4),
-        "speedup_vs_dense_sdpa": round(dense_cache[variant] / ms_call, 3),
+        "dense_sdpa_ms_per_call": round(dense_ms, 4),
+        "speedup_vs_dense_sdpa": round(dense_ms / ms_call, 3),
         "attn_fwd_ms": round(attn_ms, 4),
         "attn_fwd_tflops": round(tfs, 2),
         "mfma_frac": round(tfs / PEAK_BF16_TFLOPS, 4),
