@@ -47,6 +47,61 @@ __device__ __forceinline__ void valu_group(float (&x)[32], float& sum, uint32_t&
   (void)pk;
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// the same FLOPs as mfma_group with v_mfma_f32_16x16x32_bf16: 32 instructions of 16 cycles
+__device__ __forceinline__ void mfma16_group(f32x4 (&acc)[8], bf16x8 a, bf16x8 b) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+}
+
+// modes 4 (16x16x32 alone), 5 (16x16x32 + VALU in one wave), 6 (16x16x32 and VALU in two waves)
+template <int kMode>
+__global__ void __launch_bounds__(512, 1) overlap16_kernel(int iters, float* out) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const bool grp_mfma = wave < 4;
+  float res = 0.f;
+  if (grp_mfma) {
+    bf16x8 a, b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] = (__bf16)(0.01f * (lane + e));
+      b[e] = (__bf16)(0.02f * (lane - e));
+    }
+    f32x4 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[j][r] = 0.f;
+    float x[32];
+    float sum = 0.f;
+    uint32_t pk = 0;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) x[r] = -0.01f * (r + lane);
+    for (int it = 0; it < iters; ++it) {
+      mfma16_group(acc, a, b);
+      if (kMode == 5) valu_group(x, sum, pk);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) res += acc[j][r];
+    res += sum;
+  }
+  if (kMode == 6 && !grp_mfma) {
+    float x[32];
+    float sum = 0.f;
+    uint32_t pk = 0;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) x[r] = -0.01f * (r + lane);
+    for (int it = 0; it < iters; ++it) valu_group(x, sum, pk);
+    res += sum;
+  }
+  out[blockIdx.x * 512 + threadIdx.x] = res;
+}
+
 template <int kMode>
 __global__ void __launch_bounds__(512, 1) overlap_kernel(int iters, float* out) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -93,6 +148,21 @@ __global__ void __launch_bounds__(512, 1) overlap_kernel(int iters, float* out) 
 }
 
 template <int kMode>
+static float run16(int iters, float* d_out, int nwg) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  hipLaunchKernelGGL(overlap16_kernel<kMode>, dim3(nwg), dim3(512), 0, 0, iters, d_out);   // warm
+  (void)hipEventRecord(a);
+  for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(overlap16_kernel<kMode>, dim3(nwg), dim3(512), 0, 0, iters, d_out);
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms / 5;
+}
+
+template <int kMode>
 static float run(int iters, float* d_out, int nwg) {
   hipEvent_t a, b;
   hipEventCreate(&a);
@@ -119,6 +189,12 @@ int main(int argc, char** argv) {
   const float tv = run<1>(iters, d_out, nwg);
   const float tb = run<2>(iters, d_out, nwg);
   const float tx = run<3>(iters, d_out, nwg);
+  const float t16 = run16<4>(iters, d_out, nwg);
+  const float t16x = run16<5>(iters, d_out, nwg);
+  const float t16b = run16<6>(iters, d_out, nwg);
+  printf("{\"iters\": %d, \"mfma16_ms\": %.4f, \"mfma16_mixed_one_wave_ms\": %.4f, "
+         "\"mfma16_both_two_waves_ms\": %.4f, \"mfma16_over_mfma32\": %.3f, \"mixed16_over_mixed32\": %.3f}\n",
+         iters, t16, t16x, t16b, t16 / tm, t16x / tx);
   // per iteration and SIMD: 16 MFMAs (512 matrix cycles at 32 each) vs 80 VALU
   printf("{\"iters\": %d, \"cus\": %d, \"mfma_ms\": %.4f, \"valu_ms\": %.4f, \"both_two_waves_ms\": %.4f, "
          "\"mixed_one_wave_ms\": %.4f, \"both_over_max\": %.3f, \"both_over_sum\": %.3f, "

@@ -28,6 +28,9 @@ struct BF16 {
   static __device__ __forceinline__ f32x16 mfma32(vec8 a, vec8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   }
+  static __device__ __forceinline__ f32x4 mfma16(vec8 a, vec8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
   // bit pattern of a 16-bit element -> f32
   static __device__ __forceinline__ float bits_to_f32(uint16_t u) {
     return __uint_as_float(static_cast<uint32_t>(u) << 16);
@@ -41,6 +44,9 @@ struct F16 {
   static __device__ __forceinline__ raw from_f32(float x) { return static_cast<raw>(x); }
   static __device__ __forceinline__ f32x16 mfma32(vec8 a, vec8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x4 mfma16(vec8 a, vec8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ float bits_to_f32(uint16_t u) {
     _Float16 h;
