@@ -958,10 +958,6 @@ static int launch_fwd(const FwdParams& p, bool pool, hipStream_t stream) {
 }
 
 static int dispatch_fwd(const FwdParams& p, int D, int dtype, bool pool, hipStream_t stream) {
-  if (VB_FWD_M16 && VB_FWD_CBIAS && D == 64 && (dtype == VB_DTYPE_BF16 || dtype == VB_DTYPE_F16)) {
-    const int rc = launch_fwd_m16(p, dtype, pool, stream);
-    if (rc >= 0) return rc;
-  }
   if (dtype == VB_DTYPE_BF16) {
     if (D == 64) return launch_fwd<64, BF16>(p, pool, stream);
     if (D == 128) return launch_fwd<128, BF16>(p, pool, stream);

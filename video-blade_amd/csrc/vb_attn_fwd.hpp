@@ -96,10 +96,4 @@ struct MlTileSrc {
   int lvl;          // log2 of the level: the logit bias in the exp2 domain
 };
 
-#ifndef VB_FWD_M16
-#define VB_FWD_M16 0   // D=64 inference launches on Gilbert copies: the 16x16x32-MFMA kernel
-#endif
-// vb_attn_fwd_m16.hip: launches the 16x16x32 kernel when it covers the call, else returns -1
-int launch_fwd_m16(const FwdParams& p, int dtype, bool pool, hipStream_t stream);
-
 }  // namespace vb
