@@ -201,12 +201,25 @@ __device__ __forceinline__ void topk_wave(const float* r, int n, int keep, int32
   for (int i = lane; i < n; i += 64) sv[i] = r[i];
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
+  // the rank loop reads 4 draws per 16-byte LDS broadcast, 8 reads in flight: a one-float loop was
+  // LDS-latency bound (~6 us of sample_rows_kernel's 10 us at the CogVideoX shape)
+  const float4* s4 = reinterpret_cast<const float4*>(sv);
+  const int n4 = n >> 2;
   for (int i0 = 0; i0 < n; i0 += 64) {
     const int i = i0 + lane;
     const float v = i < n ? sv[i] : 0.f;
     int rank = 0;
-    for (int j = 0; j < n; ++j) {
-      const float w = sv[j];   // LDS broadcast
+#pragma unroll 8
+    for (int j4 = 0; j4 < n4; ++j4) {
+      const float4 w = s4[j4];
+      const int j = 4 * j4;
+      rank += (w.x > v || (w.x == v && j < i)) ? 1 : 0;
+      rank += (w.y > v || (w.y == v && j + 1 < i)) ? 1 : 0;
+      rank += (w.z > v || (w.z == v && j + 2 < i)) ? 1 : 0;
+      rank += (w.w > v || (w.w == v && j + 3 < i)) ? 1 : 0;
+    }
+    for (int j = 4 * n4; j < n; ++j) {
+      const float w = sv[j];
       rank += (w > v || (w == v && j < i)) ? 1 : 0;
     }
     if (i < n && rank < keep) dst[rank] = i;
@@ -221,7 +234,7 @@ __device__ __forceinline__ void topk_wave(const float* r, int n, int keep, int32
 // instead of two) and the first chunk of every (b,h) writes them out for the score kernel.
 template <class T>
 __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
-  __shared__ float sv[2][256];
+  __shared__ alignas(16) float sv[2][256];
   __shared__ int32_t koff_s[32];
   const int bh = blockIdx.y;
   const int wave = threadIdx.x >> 6;
@@ -578,7 +591,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
 // first). One wave per row; blockIdx.y selects the q or the k draws.
 __global__ void __launch_bounds__(256) topk_offsets_kernel(const float* rq, const float* rk, int rows, int n,
                                                            int keep, int32_t* oq, int32_t* ok) {
-  __shared__ float buf[4][256];
+  __shared__ alignas(16) float buf[4][256];
   const int wave = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows || n > 256) return;
