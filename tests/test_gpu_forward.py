@@ -348,6 +348,24 @@ def test_sample_offsets_match_torch_topk_and_rng_order():
     assert torch.equal(q_off, ref_q) and torch.equal(k_off, ref_k)
 
 
+@pytest.mark.parametrize("n,keep", [(128, 32), (131, 32), (61, 7), (256, 256)])
+def test_sample_offsets_ties_and_ragged_row_lengths(n, keep):
+    """The rank loop reads four draws per LDS broadcast with a scalar tail: rows whose length is
+    not a multiple of 4 and tie-heavy draws (a quarter of the values repeated) must still give the
+    stable descending order (ties -> lower index first, topk_wave's rule)."""
+    from vblade import ops
+    g = torch.Generator().manual_seed(n * 7 + keep)
+    r = torch.rand(2, 3, 2, n, generator=g)
+    dup = torch.rand(2, 3, 2, n, generator=g) < 0.25
+    r = torch.where(dup, torch.round(r * 8) / 8, r)              # many exact ties
+    rk = torch.rand(2, 3, 2, n, generator=g)
+    oq, ok = ops.sample_offsets(r.to(DEV), rk.to(DEV), keep)
+    want_q = torch.from_numpy(np.argsort(-r.numpy(), axis=-1, kind="stable")[..., :keep].copy())
+    want_k = torch.from_numpy(np.argsort(-rk.numpy(), axis=-1, kind="stable")[..., :keep].copy())
+    assert torch.equal(oq.cpu().long(), want_q.long())
+    assert torch.equal(ok.cpu().long(), want_k.long())
+
+
 def test_mask_predict_rejects_sequences_past_its_block_limit():
     """nb = 321 sampled blocks exceeds the predictor's LDS row buffers: a loud error, no launch."""
     L, D = 321 * 128, 64
