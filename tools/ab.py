@@ -58,6 +58,10 @@ def main():
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp,  # noqa
                                            vp=vp, kp_log_bias=math.log(m.sample_gap),
                                            heavy_rows=m.force_tail)
+        elif a.what == "fwdlse":   # the training forward's main branch (LSE out: the non-lazy kernel)
+            fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,  # noqa
+                                           heavy_rows=m.force_tail)[0]
+            fl = attn_flops(mask, L, D, 0)
         elif a.what == "pred":
             fn = lambda: m.predict_mask(q, k, qo, ko)  # noqa
         elif a.what == "bwd":   # the training-path backward (vb_attn_bwd) on the two-branch forward
@@ -94,7 +98,7 @@ def main():
                         ref = out[1].clone()
                     else:
                         print(f"  {t}: mask identical to {a.tags[0]}: {torch.equal(out[1], ref)}")
-                if a.what in ("attn", "bwd", "mlbwd"):
+                if a.what in ("attn", "fwdlse", "bwd", "mlbwd"):
                     if ref is None:
                         ref = out.float()
                     else:
@@ -113,7 +117,7 @@ def main():
         base = statistics.median(times[keys[0]])
         for kk, t in zip(keys, a.tags):
             md = statistics.median(times[kk])
-            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what in ("attn", "bwd", "mlbwd") else ""
+            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what in ("attn", "fwdlse", "bwd", "mlbwd") else ""
             print(f"{variant} {a.what} {kk}: median {md:.4f} ms (min {min(times[kk]):.4f}){extra}  "
                   f"x{base / md:.3f} vs {a.tags[0]}", flush=True)
 

@@ -65,6 +65,10 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   // q*scale to 16 bits stays within the stated tolerance; launches that return the LSE for a
   // backward keep the unscaled Q so forward and backward see the same scores.
   constexpr bool kLazy = kCBias && VB_FWD_LAZY && !VB_MFMA_ROWSUM && !VB_DIAG;
+  // s_setprio around the MFMA chains of the lazy (inference) loop: with two waves per SIMD (D=128)
+  // the wave in its MFMA phase keeps the matrix pipe fed while the other runs its softmax VALU
+  // (Wan +4 %); the LSE-returning loop and the 3-wave D=64 kernel measured slower with it
+  constexpr int kPrio = !kLazy ? 0 : D == 64 ? VB_FWD_PRIO64 : VB_FWD_PRIO128;
   constexpr float kLazyBound = std::is_same<T, BF16>::value ? kLazyBoundBF16 : kLazyBoundF16;
   constexpr int kRowB = D * 2;                 // bytes per key row
   constexpr int kMatBytes = kKT * kRowB;       // one 64-key K (or V) tile
@@ -513,6 +517,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       return max3f(a, c, fmaxf(x[7], x[15]));
     };
     auto compute_s = [&]() __attribute__((always_inline)) {
+      if constexpr (kPrio & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         typename T::vec8 kf[KS];
@@ -528,12 +533,14 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
 #pragma unroll
         for (int ks = 1; ks < KS; ++ks) s[kt] = T::mfma32(kf[ks], qf[ks], s[kt]);
       }
+      if constexpr (kPrio & 1) __builtin_amdgcn_s_setprio(0);
     };
     // P = exp2(S) of one half packed to the storage type (the PV operands of k-steps 2kt, 2kt+1)
     // WITHOUT overwriting S; returns the lane's fp32 sum (four independent chains)
     auto exp_pack = [&](const f32x16& x, typename T::vec8& p0, typename T::vec8& p1) __attribute__((always_inline)) -> float {
       float e[16];
       float h4[4];
+      if constexpr (kPrio & 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         e[r] = exp2_fast(x[r]);
@@ -547,13 +554,16 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       }
       p0 = __builtin_bit_cast(typename T::vec8, u0);
       p1 = __builtin_bit_cast(typename T::vec8, u1);
+      if constexpr (kPrio & 4) __builtin_amdgcn_s_setprio(0);
       return (h4[0] + h4[1]) + (h4[2] + h4[3]);
     };
     auto pv_pk = [&](int kk, const typename T::vec8& pf) __attribute__((always_inline)) {
       wait_v(kk);
       if (kk + VPRE < 4) read_v(kk + VPRE);
+      if constexpr (kPrio & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo[kk][dt], vhi[kk][dt]), pf, o[dt]);
+      if constexpr (kPrio & 2) __builtin_amdgcn_s_setprio(0);
     };
     // raise m by the rows' max mt of S (if > 0), rescaling O, l, the C seed and the S halves >= kt0
     // (a half whose P is already in O is dead: touching it would keep it live)
@@ -772,8 +782,10 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       wait_v(kk);
       if (kk + VPRE < 4) read_v(kk + VPRE);
       const typename T::vec8 pf = pack8<T>(s[kk >> 1], 8 * (kk & 1));
+      if constexpr (kPrio & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo[kk][dt], vhi[kk][dt]), pf, o[dt]);
+      if constexpr (kPrio & 2) __builtin_amdgcn_s_setprio(0);
 #if VB_MFMA_ROWSUM
       lsum = T::mfma32(ones, pf, lsum);
 #endif

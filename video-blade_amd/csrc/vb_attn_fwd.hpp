@@ -43,6 +43,15 @@ struct FwdParams {
 #ifndef VB_FWD_LAZY
 #define VB_FWD_LAZY 1       // inference launches: no per-tile row max (checked row sums instead)
 #endif
+// Lazy (inference) loop: s_setprio 1 around parts of the tile (bit 0: the S MFMA chain, bit 1: each
+// P.V k-step's MFMAs, bit 2: the exp/pack of a half-tile); 0 = never. `tools/ab.py --what attn`,
+// r02: the LSE-returning D=128 loop with 1 / 3 / 7 measured 1.00x / 0.97x / 0.98x (kept off there)
+#ifndef VB_FWD_PRIO64
+#define VB_FWD_PRIO64 0    // measured (CogVideoX, 3 waves per SIMD): 1 -2.6 %, 2 -0.6 %, 4 -4.1 %, 5 -6.2 %
+#endif
+#ifndef VB_FWD_PRIO128
+#define VB_FWD_PRIO128 3   // measured (Wan, 2 waves per SIMD): 3 +4.1/+4.5 %, 1 +2.5/+5.6 %, 7 +4.2 %, 2 -2.6 %, 4 +0.0 %
+#endif
 #ifndef VB_FWD_WAVES_D64
 #define VB_FWD_WAVES_D64 3  // waves per SIMD the D=64 kernel is register-budgeted for
 #endif
