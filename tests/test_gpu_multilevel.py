@@ -251,6 +251,23 @@ def test_sampler_module_with_gilbert_reorder_matches_oracle():
     assert abs(mod.sparsity_acc - 0.84375) < 1e-12
 
 
+def test_level_mask_draws_offsets_in_the_reference_rng_order():
+    """Without offsets the multi-level predictor draws rand(q) then rand(k) (efficient_attn_with_
+    pooling :77-78) and ranks them inside the sampling launch: the same scores and level mask as
+    explicit offsets from vb_sample_offsets on the same generator state."""
+    from vblade import attention, multilevel
+    B, H, L, D = 1, 3, 40 * 128 + 17, 64
+    g = torch.Generator().manual_seed(61)
+    q = torch.randn(B, H, L, D, generator=g).bfloat16().to(DEV)
+    k = torch.randn(B, H, L, D, generator=g).bfloat16().to(DEV)
+    torch.cuda.manual_seed(5)
+    po1, m1 = multilevel.predict_level_mask(q, k)
+    torch.cuda.manual_seed(5)
+    qo, ko = attention.draw_sample_offsets_qk(B, H, DEV)
+    po2, m2 = multilevel.predict_level_mask(q, k, q_off=qo, k_off=ko)
+    assert torch.equal(po1, po2) and torch.equal(m1, m2)
+
+
 # ------------------------------------------------------------------------------------- backward
 def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()

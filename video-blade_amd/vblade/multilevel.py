@@ -47,9 +47,15 @@ def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=N
     """efficient_attn_with_pooling + transfer_attn_to_mask on the (reordered through ``rows``)
     q, k: returns (po [B,H,nb,nb] q.dtype, level mask uint8 [B,H,nb,nb])."""
     B, H, L, D = q.shape
-    if q_off is None or k_off is None:
+    rand = None
+    if q_off is None and k_off is None:
+        # the reference's two draws (:77-78, q first); topk runs inside the sampling launch, as in
+        # AdaptiveBlockSparseAttn.predict_mask (one launch less than vb_sample_offsets + predict)
+        rand = (torch.rand(B, H, 1, BLOCK, device=q.device), torch.rand(B, H, 1, BLOCK, device=q.device))
+    elif q_off is None or k_off is None:
         q_off, k_off = draw_sample_offsets_qk(B, H, q.device, BLOCK, 32)
-    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, staged_event=staged_event)
+    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, staged_event=staged_event,
+                             rand=rand)
     return po, ops.level_mask(po, mask_ratios)
 
 
