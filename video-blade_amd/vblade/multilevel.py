@@ -14,7 +14,7 @@ cogvideox/sample_evaluate/modify_cogvideo.py:9):
     [B,H,nb,nb] int level mask (0 skip, 1/2/4/8 = K/V mean-pooled by that factor, +ln p logit bias).
 
 Every tensor op runs in libvblade_hip.so:
-  1. vb_sample_offsets + vb_mask_predict — sampled pooled scores (Gilbert order through ``rows``)
+  1. vb_mask_predict (the rand draws ranked inside its sampling launch) — sampled pooled scores (Gilbert order through ``rows``)
   2. vb_level_mask  — rank bands -> uint8 level mask
   3. vb_kv_pyramid  — one pass over K/V: reordered level-1 rows + 2x/4x/8x pooled rows
   4. vb_ml_attn_fwd — one softmax over every kept block's keys at its level; q rows gathered and
