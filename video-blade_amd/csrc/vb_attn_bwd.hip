@@ -624,11 +624,14 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
 // ------------------------------------------------------------------------------------------------
 // dQ: one workgroup per (b, h, 128-row q-block); kept full-resolution tiles then pooled tiles
 // ------------------------------------------------------------------------------------------------
+#ifndef VB_DQ_WAVES_D128
+#define VB_DQ_WAVES_D128 2   // D=128: two waves per SIMD with a 2-slot ring (1: one wave, 3-slot ring; Wan backward 1.014-1.018x)
+#endif
 #ifndef VB_DQ_WAVES_D64
 #define VB_DQ_WAVES_D64 2   // waves per SIMD the D=64 dQ kernel is register-budgeted for
 #endif
 template <int D, class T, bool kPool, bool kML = false>
-__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64) bwd_dq_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : VB_DQ_WAVES_D64) bwd_dq_kernel(const BwdParams p) {
   using namespace bwd;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
@@ -642,7 +645,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
   // D=128: 3-slot K/V ring, tile t is read while t+1 and t+2 are in flight, and one barrier per
   // tile both publishes tile t and proves slot (t-1) % 3 free for tile t+2 (+2 % on Wan's backward).
   // D=64: 2 slots and a second barrier per tile (the 3-slot form measured 1 % slower there).
-  constexpr int kRing = D == 128 ? 3 : 2;
+  constexpr int kRing = (D == 128 && VB_DQ_WAVES_D128 < 2) ? 3 : 2;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * kBufBytes + kMaxBlocks * 2 + 16];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kRing * kBufBytes);
   int* list_n = reinterpret_cast<int*>(smem + kRing * kBufBytes + kMaxBlocks * 2);
@@ -912,7 +915,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
       nL = -(pooled ? L2 : L1);
     }
     const float Dr = pooled ? D2 : D1;
-    if (cls != cur_cls) {   // only where the key source changes: refresh the persistent seeds
+    if (kSeedQ && cls != cur_cls) {   // only where the key source changes: refresh the persistent seeds
       asm volatile("");
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -931,7 +934,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DQ_WAVES_D64)
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks)
         s = T::mfma32(lds_b128<T>(kt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), qf[ks], s);
-      dp = T::mfma32(lds_b128<T>(vt_, dual_off<D>(kt * 32 + l32, half)), df[0], cD);
+      dp = T::mfma32(lds_b128<T>(vt_, dual_off<D>(kt * 32 + l32, half)), df[0], kSeedQ ? cD : zero);
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks)
         dp = T::mfma32(lds_b128<T>(vt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), df[ks], dp);
