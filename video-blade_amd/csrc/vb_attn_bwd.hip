@@ -627,6 +627,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
 #ifndef VB_DQ_WAVES_D128
 #define VB_DQ_WAVES_D128 2   // D=128: two waves per SIMD with a 2-slot ring (1: one wave, 3-slot ring; Wan backward 1.014-1.018x)
 #endif
+#ifndef VB_DQ_PRIO128
+#define VB_DQ_PRIO128 1   // measured (Wan backward, two waves per SIMD): 1 1.096x, 3 1.094x
+#endif
 #ifndef VB_DQ_WAVES_D64
 #define VB_DQ_WAVES_D64 2   // waves per SIMD the D=64 dQ kernel is register-budgeted for
 #endif
@@ -878,6 +881,8 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
   const bool many = wave < (kInst & 3);
 
   constexpr bool kSeedQ = D == 64 || VB_BWD_SEED128;
+  // s_setprio 1 around the MFMA chains (bit 0: S and dP, bit 1: the dQ steps) at D=128
+  constexpr int kPrioQ = D == 128 ? VB_DQ_PRIO128 : 0;
   f32x16 cD, zero;
 #pragma unroll
   for (int r = 0; r < 16; ++r) cD[r] = zero[r] = 0.f;
@@ -930,6 +935,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
       // dP^T's chain starts from cD = -Delta of the lane's row (dS = P * (dO.V^T - Delta) with no
       // subtraction per score); the seeds are persistent registers read as the MFMA's C operand
       f32x16 s, dp;
+      if constexpr (kPrioQ & 1) __builtin_amdgcn_s_setprio(1);
       s = T::mfma32(lds_b128<T>(kt_, dual_off<D>(kt * 32 + l32, half)), qf[0], zero);
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks)
@@ -938,6 +944,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
 #pragma unroll
       for (int ks = 1; ks < KS; ++ks)
         dp = T::mfma32(lds_b128<T>(vt_, dual_off<D>(kt * 32 + l32, 2 * ks + half)), df[ks], dp);
+      if constexpr (kPrioQ & 1) __builtin_amdgcn_s_setprio(0);
       if (klen < kT) {
         asm volatile("");
 #pragma unroll
@@ -966,6 +973,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
         rk[slot][1] = lds_tr4_asm_at(kt_, dual_off_col<D>(rr + 8, cc));
       };
       rd(0, 0);
+      if constexpr (kPrioQ & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < NST; ++j) {
         const int sl = j & 1;
@@ -977,6 +985,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
         }
         dq[j % DT] = T::mfma32(join8<T>(rk[sl][0], rk[sl][1]), pdv[j / DT], dq[j % DT]);
       }
+      if constexpr (kPrioQ & 2) __builtin_amdgcn_s_setprio(0);
     }
     if (kRing == 2) __builtin_amdgcn_s_barrier();   // slot t % 2 is refilled by the next issue
   };
