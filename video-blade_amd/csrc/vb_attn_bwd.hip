@@ -177,12 +177,20 @@ __global__ void __launch_bounds__(256) bwd_prep_kernel(const PrepParams p) {
 #ifndef VB_BWD_SEED128
 #define VB_BWD_SEED128 0    // D=128: dP seeded with -Delta too (measured 6 % slower on Wan's dK/dV)
 #endif
+#ifndef VB_DKDV_PRIO64
+#define VB_DKDV_PRIO64 1   // measured (cog backward): 1 1.013x, 3 1.009x
+#endif
+#ifndef VB_DKDV_PRIO128
+#define VB_DKDV_PRIO128 0  // one wave per SIMD at D=128: nothing to arbitrate
+#endif
 #ifndef VB_DKDV_WAVES_D64
 #define VB_DKDV_WAVES_D64 2   // waves per SIMD the D=64 dK/dV kernel is register-budgeted for
 #endif
 template <int D, class T, bool kPooled, bool kML = false>
 __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D64) bwd_dkdv_kernel(const BwdParams p) {
   using namespace bwd;
+  // s_setprio 1 around the MFMA chains (bit 0: S and dP, bit 1: the dV/dK steps)
+  constexpr int kPrioKV = D == 128 ? VB_DKDV_PRIO128 : VB_DKDV_PRIO64;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
   constexpr int RB = D * 2;                 // bytes per row
@@ -426,12 +434,14 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
           dp[4 * j + e] = kSeed ? Dv[e] : 0.f;
         }
       }
+      if constexpr (kPrioKV & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         s = T::mfma32(lds_b128<T>(qt, dual_off<D>(32 * u + l32, 2 * ks + half)), kf[ks], s);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         dp = T::mfma32(lds_b128<T>(dot, dual_off<D>(32 * u + l32, 2 * ks + half)), vf[ks], dp);
+      if constexpr (kPrioKV & 1) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 Lv = *reinterpret_cast<const f32x4*>(st + fL * 64 + 32 * u + 8 * j + 4 * half);
@@ -467,6 +477,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
         rq[slot][1] = lds_tr4_asm_at(qt, dual_off_col<D>(rr + 8, cc));
       };
       rd(0, 0);
+      if constexpr (kPrioKV & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < NST; ++j) {
         const int sl = j & 1;
@@ -480,6 +491,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
         dv[dt] = T::mfma32(join8<T>(rdo[sl][0], rdo[sl][1]), pp[sb], dv[dt]);
         dk[dt] = T::mfma32(join8<T>(rq[sl][0], rq[sl][1]), pd[sb], dk[dt]);
       }
+      if constexpr (kPrioKV & 2) __builtin_amdgcn_s_setprio(0);
     }
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
@@ -626,6 +638,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
 // ------------------------------------------------------------------------------------------------
 #ifndef VB_DQ_WAVES_D128
 #define VB_DQ_WAVES_D128 2   // D=128: two waves per SIMD with a 2-slot ring (1: one wave, 3-slot ring; Wan backward 1.014-1.018x)
+#endif
+#ifndef VB_DQ_PRIO64
+#define VB_DQ_PRIO64 0     // measured (cog backward): 1 0.990x, 3 0.990x
 #endif
 #ifndef VB_DQ_PRIO128
 #define VB_DQ_PRIO128 1   // measured (Wan backward, two waves per SIMD): 1 1.096x, 3 1.094x
@@ -882,7 +897,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
 
   constexpr bool kSeedQ = D == 64 || VB_BWD_SEED128;
   // s_setprio 1 around the MFMA chains (bit 0: S and dP, bit 1: the dQ steps) at D=128
-  constexpr int kPrioQ = D == 128 ? VB_DQ_PRIO128 : 0;
+  constexpr int kPrioQ = D == 128 ? VB_DQ_PRIO128 : VB_DQ_PRIO64;
   f32x16 cD, zero;
 #pragma unroll
   for (int r = 0; r < 16; ++r) cD[r] = zero[r] = 0.f;
