@@ -269,7 +269,10 @@ def run(args):
     sparsity = mod.sparsity_acc / mod.sparsity_counter if ml else mod.sparsity
 
     result = {
-        "metric": "frames/sec/GPU, " + V["name"] + " (attention path); attn TFLOPS vs dense",
+        # `value` is the whole-job aggregate over all ranks (the driver's contract); BASELINE's
+        # per-GPU figure is per_gpu_frames_per_s = value / n_gpus (equal at N=1)
+        "metric": "frames/sec (aggregate over n_gpus; per GPU = value/n_gpus), " + V["name"]
+                  + " (attention path); attn TFLOPS vs dense",
         "value": round(value, 4),
         "unit": "frames/s",
         "n_gpus": world,

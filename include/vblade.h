@@ -199,6 +199,11 @@ int vb_lse_combine(const void* out1, const float* lse1, const void* out2, const 
  * q/out/out2/dout/lse/lse2/alpha/dq rows are addressed through q_rows[g] like vb_attn_fwd; dk/dv of
  * reordered key g are written at row kv_rows[g] (NULL = g). dq/dk/dv are fully overwritten.
  * `workspace` (device, 16-byte aligned) of at least vb_attn_bwd_workspace_size(args) bytes.
+ * The workspace grows linearly with B: besides the per-row statistics and the reordered q/dO
+ * copies it holds the pooled-key dK/dV partials, psplit * B * H * Lkp * D fp32 values twice, with
+ * psplit chosen from H and L only (never B) so that a sample's gradients are the same bits alone
+ * or inside a micro-batch. At B=5 that is ~0.86 GB for CogVideoX (psplit 6) and ~1.9 GB for Wan
+ * (psplit 14) — small against 288 GB of HBM, so no cap is applied.
  * ------------------------------------------------------------------------------------------ */
 typedef struct vb_attn_bwd_args {
   const void* q; int64_t q_stride[3];

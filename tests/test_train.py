@@ -1,7 +1,7 @@
 """CPU: the TDM training-step integration (vblade.train) — LoRA layers, gradient checkpointing,
 the bucketed data-parallel gradient all-reduce (gloo, world size 2) and the diffusers LoRA
 checkpoint format. The attention inside is a CPU stand-in here (plain softmax attention); the
-GPU test (test_gpu_module.py) runs the same step through the HIP sparse attention."""
+GPU tests (test_gpu_train.py) run TrainStep and TDMTrainStep through the HIP sparse attention."""
 import os
 import socket
 

@@ -4,7 +4,6 @@ ONE GPU: the same inputs, launches interleaved A,B,A,B,... so clock/device drift
 usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred|call]"""
 import argparse
 import ctypes
-import math
 import os
 import statistics
 import sys
@@ -56,7 +55,7 @@ def main():
         fl = attn_flops(mask, L, D, kp.shape[2])
         if a.what == "attn":
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp,  # noqa
-                                           vp=vp, kp_log_bias=math.log(m.sample_gap),
+                                           vp=vp, kp_log_bias=m._log_gap(q.dtype),
                                            heavy_rows=m.force_tail)
         elif a.what == "fwdlse":   # the training forward's main branch (LSE out: the non-lazy kernel)
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,  # noqa
@@ -74,7 +73,7 @@ def main():
             _, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
             fn = lambda: ops.attention_bwd(do, q, k_r, v_r, out1, lse1, block_mask=mask, q_rows=rows,  # noqa
                                            kv_rows=rows, kp=kp, vp=vp, out2=out2, lse2=lse2,
-                                           alpha=alpha, gap=gap, heavy_rows=m.force_tail)[0]
+                                           alpha=alpha, gap=gap, heavy_rows=m.force_tail)
             fl = 2.5 * fl
         elif a.what == "mlbwd":   # the multi-level path's backward (vb_ml_attn_bwd), dk compared
             from vblade import multilevel
@@ -99,11 +98,14 @@ def main():
                     else:
                         print(f"  {t}: mask identical to {a.tags[0]}: {torch.equal(out[1], ref)}")
                 if a.what in ("attn", "fwdlse", "bwd", "mlbwd"):
+                    outs = tuple(out) if isinstance(out, tuple) else (out,)   # bwd: dq, dk, dv
                     if ref is None:
-                        ref = out.float()
+                        ref = tuple(o.clone() for o in outs)
                     else:
-                        err = (out.float() - ref).abs().max().item()
-                        print(f"  {t}: max|out - {a.tags[0]}| = {err:.3e}")
+                        same = all(torch.equal(o, r) for o, r in zip(outs, ref))
+                        err = max((o.float() - r.float()).abs().max().item() for o, r in zip(outs, ref))
+                        print(f"  {t}: bit-identical to {a.tags[0]} over {len(outs)} output(s): {same}; "
+                              f"max|diff| = {err:.3e}")
             for _ in range(a.rounds):
                 for kk, t in zip(keys, a.tags):
                     _lib._lib = libs[t]

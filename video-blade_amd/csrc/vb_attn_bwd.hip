@@ -660,9 +660,10 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
   constexpr int kCh = RB / 16;
   constexpr int kInst = 2 * kInstTile;
   constexpr int kBufBytes = 2 * kTileBytes;
-  // D=128: 3-slot K/V ring, tile t is read while t+1 and t+2 are in flight, and one barrier per
-  // tile both publishes tile t and proves slot (t-1) % 3 free for tile t+2 (+2 % on Wan's backward).
-  // D=64: 2 slots and a second barrier per tile (the 3-slot form measured 1 % slower there).
+  // 2-slot K/V ring with a second barrier per tile: D=64, and D=128 at the default two waves per
+  // SIMD (VB_DQ_WAVES_D128=2, 68 KiB). Only the one-wave D=128 build (VB_DQ_WAVES_D128=1) takes a
+  // 3-slot ring, where tile t is read while t+1 and t+2 are in flight and one barrier per tile both
+  // publishes tile t and proves slot (t-1) % 3 free for tile t+2.
   constexpr int kRing = (D == 128 && VB_DQ_WAVES_D128 < 2) ? 3 : 2;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * kBufBytes + kMaxBlocks * 2 + 16];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kRing * kBufBytes);

@@ -7,13 +7,14 @@ cogvideo_blocksparseattn.py:398-427; wanx_blocksparseattn.py:375-409) and its he
 (:9-16) as constructor arguments. Every tensor op of the hot path runs in libvblade_hip.so:
 
   forward (inference, the 8-step samplers):
-    1. vb_mask_predict  — sampled pooled scores + energy top-k -> block mask (Gilbert order)
-    2. vb_pool_kv       — mean-pooled K/V over `sample_gap` reordered tokens
-    3. vb_attn_fwd      — ONE softmax over kept full-res keys ∪ pooled keys (+ln gap bias):
+    1. vb_mask_predict  — sampled pooled scores + energy top-k -> block mask (Gilbert order); the
+                          pooled K/V pass (mean over `sample_gap` reordered tokens) runs in the
+                          same launch as extra workgroups (one stream, no events)
+    2. vb_attn_fwd      — ONE softmax over kept full-res keys ∪ pooled keys (+ln gap bias):
                           the reference's two attention calls + LSE combine, fused; q/k/v rows
                           gathered and out rows scattered through the Gilbert index (no copies)
   training (grad required) keeps the reference's two-branch structure so the backward has the
-  reference's semantics (LSE/alpha detached): see ``ops_autograd.AdaptiveSplitAttention``.
+  reference's semantics (LSE/alpha detached): see ``autograd.adaptive_split_attention``.
 
 Only the tiny RNG draw of the sampling offsets (torch.rand + topk over [B,H,1,128], exactly as
 cogvideo_blocksparseattn.py:45-46 so the RNG stream matches the reference) stays in PyTorch.
@@ -144,7 +145,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
         # optional list: when set, every fused attention launch is bracketed by a pair of HIP
         # events on the launch stream (bench.py's live kernel timing); None = no events
         self.attn_events: Optional[list] = None
-        # overlap the pooled K/V pass with the predictor on a second stream (inference only)
+        # run the pooled K/V pass inside the predictor's launch (extra workgroups beside the score
+        # workgroups, one stream) instead of as its own launch after it (inference only)
         self.overlap = bool(cfg.get("overlap", True))
         # The attention kernel gathers K/V rows through the Gilbert index (True) or streams the
         # Gilbert-ordered contiguous copies the pooled pass writes (False: 2·L·D·2 bytes more per
@@ -152,7 +154,6 @@ class AdaptiveBlockSparseAttn(nn.Module):
         # head dim (tools/overlap_ab.py --opt gather_kv): gather at D=128 (Wan, +2.4 % per call),
         # copies at D=64 (CogVideoX, +0.9 %).
         self.gather_kv = cfg.get("gather_kv", "auto")
-        self._side = ops.SideStream()
 
     # -------------------------------------------------------------------------------- helpers
     def _rows(self, device):
@@ -264,7 +265,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self.last_mask = mask
         if not fused:
             from .autograd import adaptive_split_attention
-            out = adaptive_split_attention(q, k, v, mask, rows, self.sample_gap)
+            out = adaptive_split_attention(q, k, v, mask, rows, self.sample_gap,
+                                           heavy_rows=self.force_tail)
         else:
             # q rows gathered and out rows scattered inside the attention kernel
             if len(pooled) == 4:   # Gilbert-ordered copies: streamed contiguously

@@ -53,15 +53,16 @@ def block_sparse_attn_func(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k
 
 class _AdaptiveSplitFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, mask, rows, gap):
+    def forward(ctx, q, k, v, mask, rows, gap, heavy_rows):
         kp, vp, k_r, v_r = ops.pool_kv(k, v, gap, rows, reordered=True)
         out1, lse1 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,
-                                       heavy_rows=2)
+                                       heavy_rows=heavy_rows)
         out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
                                        need_lse=True)
         out, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
         ctx.save_for_backward(q, k_r, v_r, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp)
         ctx.gap = gap
+        ctx.heavy_rows = heavy_rows
         return out
 
     @staticmethod
@@ -71,9 +72,10 @@ class _AdaptiveSplitFn(torch.autograd.Function):
         # through the mean pool and the Gilbert gather, returned in the caller's row order
         dq, dk, dv = ops.attention_bwd(dout.contiguous(), q, k_r, v_r, out1, lse1, block_mask=mask,
                                        q_rows=rows, kv_rows=rows, kp=kp, vp=vp, out2=out2,
-                                       lse2=lse2, alpha=alpha, gap=ctx.gap, heavy_rows=2)
-        return dq, dk, dv, None, None, None
+                                       lse2=lse2, alpha=alpha, gap=ctx.gap, heavy_rows=ctx.heavy_rows)
+        return dq, dk, dv, None, None, None, None
 
 
-def adaptive_split_attention(q, k, v, mask, rows, gap):
-    return _AdaptiveSplitFn.apply(q, k, v, mask, rows, gap)
+def adaptive_split_attention(q, k, v, mask, rows, gap, heavy_rows=2):
+    """heavy_rows: forced-dense tail rows dispatched first (CogVideoX 2, Wan 0); scheduling only."""
+    return _AdaptiveSplitFn.apply(q, k, v, mask, rows, gap, heavy_rows)

@@ -457,10 +457,10 @@ def kv_pyramid(k, v, rows=None, stream=None, out=None):
     level-1 rows (zero beyond L), then the 2x, 4x, 8x mean-pooled rows (replicate padding).
     ``stream``: as pool_kv."""
     if v.shape != k.shape:
-        raise ValueError(f"pool_kv: k and v must have the same shape, got {tuple(k.shape)} and "
+        raise ValueError(f"kv_pyramid: k and v must have the same shape, got {tuple(k.shape)} and "
                          f"{tuple(v.shape)}")
     if rows is not None and rows.numel() != k.shape[2]:
-        raise ValueError(f"pool_kv: rows has {rows.numel()} entries for {k.shape[2]} keys")
+        raise ValueError(f"kv_pyramid: rows has {rows.numel()} entries for {k.shape[2]} keys")
     dev = _require_gpu(k, v, rows)
     k, v = _aligned_bhld(k), _aligned_bhld(v)
     if stream is not None:   # see pool_kv
