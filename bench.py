@@ -559,22 +559,39 @@ def measure_backward(variant, dev, reps=6):
 
 
 def quality_vs_oracle(mod, qkv, variant):
-    """Head 0 of one call of the timed configuration against the oracle's reference-faithful
-    adaptive path (two branches + bf16 combine) with the GPU's own mask (SURVEY §8d Quality)."""
+    """Head 0 of one call of the timed configuration against the oracle with the GPU's own mask
+    (SURVEY §8d Quality): PSNR, max|err| and the bf16 ULP histogram against (a) the reference's
+    rounding (two branches, lse cast to bf16, bf16 combine: adaptive_attention) and (b) the exact
+    fp64 joint softmax of the same two branches (joint_from_branches), and the reference's own
+    distance from (b)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import bsa_oracle as O
     q, k, v = qkv
     out = mod(q, k, v)
     mask = mod.last_mask[:, :1].bool().cpu()
     cfg = O.AdaptiveConfig.cogvideox() if variant == "cog" else O.AdaptiveConfig.wan()
-    ref = O.adaptive_attention(q[:, :1].cpu(), k[:, :1].cpu(), v[:, :1].cpu(), cfg, None, None,
-                               mask=mask, store_dtype=torch.bfloat16)["out"]
+    fwd = O.adaptive_attention(q[:, :1].cpu(), k[:, :1].cpu(), v[:, :1].cpu(), cfg, None, None,
+                               mask=mask, store_dtype=torch.bfloat16)
+    ref = fwd["out"]
+    exact = O.joint_from_branches(fwd, mod._log_gap(torch.bfloat16))
     got = out[:, :1].float().cpu()
-    mse = torch.mean((got.double() - ref.double()) ** 2).item()
-    peak = ref.abs().max().item()
-    return {"head": 0, "psnr_db": round(10 * math.log10(peak * peak / max(mse, 1e-30)), 2),
+
+    def psnr(a, b):
+        mse = torch.mean((a.double() - b.double()) ** 2).item()
+        peak = b.double().abs().max().item()
+        return round(10 * math.log10(peak * peak / max(mse, 1e-30)), 2)
+
+    h_ref, h_ex, h_re = (O.bf16_ulp_histogram(a, b) for a, b in ((got, ref), (got, exact), (ref, exact)))
+    return {"head": 0, "psnr_db": psnr(got, ref),
             "max_abs": round((got - ref).abs().max().item(), 5),
-            "vs": "oracle/bsa_oracle.adaptive_attention (reference rounding), same mask"}
+            "ulp_hist": h_ref["ulp_hist"], "max_ulp": h_ref["max_ulp"],
+            "vs": "oracle/bsa_oracle.adaptive_attention (reference rounding), same mask",
+            "vs_exact": {"psnr_db": psnr(got, exact),
+                         "max_abs": round((got.double() - exact).abs().max().item(), 5),
+                         "ulp_hist": h_ex["ulp_hist"], "max_ulp": h_ex["max_ulp"],
+                         "vs": "oracle joint_from_branches: the same branches combined exactly (fp64)"},
+            "reference_vs_exact": {"max_abs": round((ref.double() - exact).abs().max().item(), 5),
+                                   "ulp_hist": h_re["ulp_hist"], "max_ulp": h_re["max_ulp"]}}
 
 
 def pmc_traffic(variant, timeout=300):

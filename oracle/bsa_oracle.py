@@ -404,6 +404,48 @@ def adaptive_attention_joint(q, k, v, cfg: AdaptiveConfig, mask):
     return out_r[:, :, inv], lse
 
 
+def joint_from_branches(fwd: dict, log_gap: float) -> torch.Tensor:
+    """Exact (fp64) single-softmax combine of ``adaptive_attention``'s unrounded branch results
+    (out1/lse1, out2/lse2): the a9 identity with no bf16 rounding of lse, alpha or the branch
+    outputs, the pooled keys carrying the bias ``log_gap`` (the reference's combine uses the bf16
+    value of ln g, :375-376). Returns the output in the original token order (fp64)."""
+    l1 = fwd["lse1"].double()
+    l2 = fwd["lse2"].double() + log_gap
+    lse = torch.logaddexp(l1, l2)
+    a = torch.exp(l1 - lse)[..., None]
+    out_r = fwd["out1"].double() * a + fwd["out2"].double() * (1 - a)
+    P = fwd["perm"]
+    inv = torch.empty_like(P)
+    inv[P] = torch.arange(P.numel())
+    return out_r[:, :, inv]
+
+
+def bf16_ulp_distance(got: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
+    """Checker utility: distance in bf16 units in the last place between got and ref, both
+    rounded to bf16 (round to nearest even), counted on the monotone integer image of the bit
+    patterns (so it is exact across binades and signs). int64 tensor of got's shape."""
+    def ordered(x):
+        b = x.to(torch.bfloat16).view(torch.int16).to(torch.int64)
+        return torch.where(b < 0, -(b & 0x7FFF), b)
+    return (ordered(got.float()) - ordered(ref.float())).abs()
+
+
+ULP_BUCKETS = ((0, 0), (1, 1), (2, 2), (3, 4), (5, 8), (9, 16), (17, None))
+
+
+def bf16_ulp_histogram(got: torch.Tensor, ref: torch.Tensor) -> dict:
+    """Fractions of elements per bf16-ULP distance bucket (0, 1, 2, 3-4, 5-8, 9-16, >16), plus
+    the maximum distance (SURVEY §8d Quality)."""
+    d = bf16_ulp_distance(got, ref).flatten()
+    n = d.numel()
+    hist = {}
+    for lo, hi in ULP_BUCKETS:
+        sel = (d >= lo) if hi is None else ((d >= lo) & (d <= hi))
+        key = f">{lo - 1}" if hi is None else (str(lo) if lo == hi else f"{lo}-{hi}")
+        hist[key] = round(int(sel.sum()) / n, 6)
+    return {"ulp_hist": hist, "max_ulp": int(d.max()), "n": n}
+
+
 def adaptive_attention_bwd(q, k, v, dout, cfg: AdaptiveConfig, fwd: dict):
     """Gradient of adaptive_attention w.r.t. q, k, v under the reference's autograd semantics
     (a10): mask under no_grad; LSEs carry no gradient (FA2 convention) so alpha is a constant;

@@ -158,6 +158,41 @@ def test_fused_sampling_and_pool_launches_match_separate_launches(variant, D):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("variant,D,B,H,strided", [("cog", 64, 1, 3, False), ("cog", 64, 2, 2, True),
+                                                     ("wan", 128, 1, 2, False), ("wan", 128, 2, 1, True)])
+def test_inloop_pooled_pass_matches_pool_kv_at_full_length(variant, D, B, H, strided):
+    """At the real sequence lengths the pooled K/V pass runs INSIDE the score kernel's loop (one
+    source row per thread and K tile, vb_predict.hip kPoolIn): pooled K/V and the Gilbert-order
+    copies must equal the stand-alone vb_pool_kv bit for bit, and the mask must equal the predictor
+    run without the pass. Batched and on the processors' strided [B,L,H,D].transpose(1,2) views."""
+    import vblade
+    from vblade import ops
+    m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+    L = m.gilbert_rearranger.seq_len
+    g = torch.Generator(device=DEV).manual_seed(77)
+    shape = (B, L, H, D) if strided else (B, H, L, D)
+    q, k, v = (torch.randn(*shape, generator=g, device=DEV).bfloat16() for _ in range(3))
+    if strided:
+        q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    rows = m._rows(q.device)
+    rq = torch.rand(B, H, 1, 128, device=DEV, generator=g)
+    rk = torch.rand(B, H, 1, 128, device=DEV, generator=g)
+    with torch.no_grad():
+        for copies in (True, False):
+            outs = ops.pool_kv_outputs(k, m.sample_gap, reordered=copies)
+            po_p, mask_p = ops.mask_predict(q, k, rows=rows, energy_threshold=0.95, min_keep=6,
+                                            max_keep=13, force_tail=m.force_tail, rand=(rq, rk),
+                                            pool=(v, m.sample_gap, outs))
+            po_r, mask_r = ops.mask_predict(q, k, rows=rows, energy_threshold=0.95, min_keep=6,
+                                            max_keep=13, force_tail=m.force_tail, rand=(rq, rk))
+            ref = ops.pool_kv(k, v, m.sample_gap, rows, reordered=copies)
+            torch.cuda.synchronize()
+            assert torch.equal(mask_p, mask_r) and torch.equal(po_p, po_r)
+            assert len(outs) == len(ref)
+            for a, b in zip(outs, ref):
+                assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("variant,D", [("cog", 64), ("wan", 128)])
 def test_gathered_kv_rows_equal_gilbert_copies(variant, D):
     """The attention kernel gathering K/V rows through the Gilbert index (gather_kv=True) and

@@ -187,6 +187,31 @@ def test_tdm_step_updates_both_models_and_fake_starts_as_student():
     assert step.opt_g.defaults["betas"] == (0.0, 0.95) and step.opt_d.defaults["betas"] == (0.0, 0.95)
 
 
+def test_tdm_default_teacher_is_dense_unpatched_base_with_cfg():
+    """The reference's teacher is loaded separately and never patched (train_cogvideo_tdm.py:
+    1014-1022; the sparse patch at :997-1000 is the student's) and runs classifier-free guidance
+    (:1712, :1487-1498); the fake model is a deep copy of the (patched) student (:1301)."""
+    student, base = _tdm_models()
+    step = T.TDMTrainStep(student, lr=1e-2, lr_fake=1e-2, accum=1, cfg=3.5)
+    blk = step.teacher.transformer_blocks[0]
+    assert isinstance(blk.inner_attention, T.DenseAttention)
+    assert not isinstance(student.transformer_blocks[0].inner_attention, T.DenseAttention)
+    assert type(step.fake.transformer_blocks[0].inner_attention) is type(student.transformer_blocks[0].inner_attention)
+    assert all(not p.requires_grad for p in step.teacher.parameters())
+    for (n, a), b in zip(step.teacher.named_parameters(), base.parameters()):
+        assert torch.equal(a, b), n          # base weights, LoRA B zero: no adapter
+    x = torch.randn(2, 32, 64)
+    cond = torch.randn(2, 1, 64)
+    with torch.no_grad():
+        got = step.teacher_predict(x, cond)
+        c = step.teacher(x, cond)
+        u = step.teacher(x, step.uncond)
+    assert torch.allclose(got, u + 3.5 * (c - u))
+    assert abs(step.huber_c - 1e-3 / ((64 * 64 * 4) ** 0.5 * (60 * 90 * 16 * 13) ** 0.5)) < 1e-20
+    lf, lg = step([_tdm_batches(1, 2)[0] + (cond,)])
+    assert torch.isfinite(lf) and torch.isfinite(lg)
+
+
 def _tdm_dp_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -105,7 +105,11 @@ class StandInTransformer(nn.Module):
                                    generator=g) for _ in range(num_layers)])
         self.gradient_checkpointing = gradient_checkpointing
 
-    def forward(self, x):
+    def forward(self, x, cond: Optional[torch.Tensor] = None):
+        """``cond``: the stand-in for the prompt embedding (encoder_hidden_states), added to the
+        input; the classifier-free-guidance pair runs the model once per embedding."""
+        if cond is not None:
+            x = x + cond.to(x.dtype)
         for blk in self.transformer_blocks:
             if self.gradient_checkpointing and torch.is_grad_enabled():
                 x = checkpoint(blk, x, use_reentrant=False)
@@ -115,6 +119,38 @@ class StandInTransformer(nn.Module):
 
     def lora_parameters(self) -> List[nn.Parameter]:
         return [p for p in self.parameters() if p.requires_grad]
+
+
+class DenseAttention(nn.Module):
+    """The unpatched attention of a diffusers CogVideoX block: dense
+    F.scaled_dot_product_attention over [B,H,L,D] (what the TDM teacher runs: the reference loads
+    ``transformer_real`` separately and never patches it, train_cogvideo_tdm.py:1014-1022 vs the
+    student-only patch at :997-1000)."""
+
+    def forward(self, q, k, v):
+        return F.scaled_dot_product_attention(q, k, v)
+
+
+def dense_copy(model: StandInTransformer) -> StandInTransformer:
+    """A frozen copy of ``model``'s base weights (LoRA B zeroed, i.e. no adapter) with dense
+    attention: the TDM teacher (transformer_real, from_pretrained without LoRA, requires_grad
+    False)."""
+    import copy
+    t = copy.deepcopy(model)
+    dense = DenseAttention()
+    for blk in t.transformer_blocks:
+        blk.inner_attention = dense
+    with torch.no_grad():
+        for n, p in t.named_parameters():
+            if n.endswith("lora_B"):
+                p.zero_()
+            p.requires_grad_(False)
+    return t
+
+
+# the generator loss's pseudo-Huber constant, as the reference overwrites it before the loss
+# (train_cogvideo_tdm.py:1723): 1e-3 / (sqrt(64*64*4) * sqrt(60*90*16*13)) ~= 7.4e-9
+HUBER_C_REF = 1e-3 / (((64 * 64 * 4) ** 0.5) * (60 * 90 * 16 * 13) ** 0.5)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -257,36 +293,43 @@ class TrainStep:
 class TDMTrainStep:
     """The TDM joint step with its two trained models (train_cogvideo_tdm.py:1301-1325, loop
     :1640-1737): a student (the K-step generator) and a fake-score model initialised as a deep copy
-    of it (:1301), each with its own AdamW (betas (0, 0.95): ``args.adam_beta1 = 0`` at :1310),
-    learning rate, gradient clipping and data-parallel gradient exchange (two accelerators,
-    :1318-1325), plus a frozen teacher ("real" model). Every micro-batch runs, in the reference's
-    order:
+    of it (:1301, so it carries the student's sparse attention and LoRA), each with its own AdamW
+    (betas (0, 0.95): ``args.adam_beta1 = 0`` at :1310), learning rate, gradient clipping and
+    data-parallel gradient exchange (two accelerators, :1318-1325), plus a frozen teacher ("real"
+    model) with DENSE attention and no LoRA (loaded separately and never patched, :1014-1022;
+    ``dense_copy`` of the student by default). Every micro-batch runs, in the reference's order:
 
     1. fake-score update (:1640-1688): the student's prediction without grad, the fake model's
        prediction WITH grad (sparse attention under autograd), the weighted regression loss
        ``mean(w * (fake - student)^2)``, backward into the fake model;
-    2. generator update (:1690-1737): the student's prediction WITH grad, teacher and fake
-       predictions without grad, the revised target ``student + real - fake`` (detached), the
-       pseudo-Huber loss over ``weighting_factor`` (:1719-1727), backward into the student.
+    2. generator update (:1690-1737): the student's prediction WITH grad; the teacher with
+       classifier-free guidance (predictor.predict(..., cfg=args.cfg) :1712, :1487-1498: one pass
+       on the prompt embedding, one on the unconditional embedding, uncond + cfg * (cond -
+       uncond); cfg 3.5 in train_tdm_1.sh) and the fake model without grad; the revised target
+       ``student + real - fake`` (detached), the pseudo-Huber loss over ``weighting_factor`` with
+       the reference's c (:1719-1727), backward into the student.
 
     On the last micro-batch of an accumulation window each model's reducer exchanges its LoRA
     gradients (one bucketed all-reduce per model), then clip + AdamW per model. The diffusion
     specifics (noise schedules, timesteps, K-step ODE states) are outside the hot path: a
     micro-batch gives the student's input ``x_gen`` (the noisy ODE state), the re-noised input the
-    fake and teacher models see ``x_noisy`` (noisy_model_latents) and the regression weight ``w``
-    (1 / (1 - alphas_cumprod[t])). The three models share nothing; each
-    carries its own sparse-attention module (a deep copy, as at :1301)."""
+    fake and teacher models see ``x_noisy`` (noisy_model_latents), the regression weight ``w``
+    (1 / (1 - alphas_cumprod[t])) and optionally the prompt embedding ``cond`` (the stand-in adds
+    it to the input; zeros if absent). The unconditional embedding is ``uncond`` (fixed)."""
 
     def __init__(self, student: StandInTransformer, teacher: Optional[StandInTransformer] = None, *,
                  lr: float = 1e-4, lr_fake: float = 1e-4, betas=(0.0, 0.95), weight_decay: float = 1e-4,
                  eps: float = 1e-8, max_grad_norm: float = 1.0, accum: int = 1, group=None,
-                 bucket_bytes: int = 64 << 20, huber_c: float = 1e-3, distributed: Optional[bool] = None):
+                 bucket_bytes: int = 64 << 20, huber_c: float = HUBER_C_REF, cfg: Optional[float] = 3.5,
+                 uncond: Optional[torch.Tensor] = None, distributed: Optional[bool] = None):
         import copy
         self.student = student
+        self.teacher = teacher if teacher is not None else dense_copy(student)
         self.fake = copy.deepcopy(student)
-        self.teacher = teacher if teacher is not None else copy.deepcopy(student)
         for q in self.teacher.parameters():
             q.requires_grad_(False)
+        self.cfg = cfg
+        self.uncond = uncond
         self.accum = accum
         self.max_grad_norm = max_grad_norm
         self.huber_c = huber_c
@@ -312,18 +355,35 @@ class TDMTrainStep:
         opt.zero_grad(set_to_none=True)
         return gnorm
 
+    def _uncond_like(self, x):
+        if self.uncond is None:
+            g = torch.Generator().manual_seed(1234)
+            self.uncond = torch.randn(1, 1, x.shape[-1], generator=g) * 0.5
+        return self.uncond.to(device=x.device, dtype=x.dtype)
+
+    def teacher_predict(self, x_noisy, cond):
+        """predictor.predict(transformer_real, ..., cfg=args.cfg) (:1712, :1475-1498): with cfg,
+        uncond + cfg * (cond - uncond) of the conditional and unconditional passes."""
+        real = self.teacher(x_noisy, cond)
+        if self.cfg is None:
+            return real
+        real_u = self.teacher(x_noisy, self._uncond_like(x_noisy))
+        return real_u + self.cfg * (real - real_u)
+
     def __call__(self, micro_batches: List[tuple]):
-        """micro_batches: ``accum`` tuples (x_gen, x_noisy, w). Returns (loss_fake, loss_gen)."""
+        """micro_batches: ``accum`` tuples (x_gen, x_noisy, w[, cond]). Returns (loss_fake, loss_gen)."""
         assert len(micro_batches) == self.accum
         lf, lg = [], []
-        for i, (x_gen, x_noisy, w) in enumerate(micro_batches):
+        for i, mb in enumerate(micro_batches):
+            x_gen, x_noisy, w = mb[:3]
+            cond = mb[3] if len(mb) > 3 else None
             last = i == self.accum - 1
             # 1. fake-score update
             if self.red_d is not None:
                 self.red_d.enable(last)
             with torch.no_grad():
-                target = self.student(x_gen)
-            fake = self.fake(x_noisy)
+                target = self.student(x_gen, cond)
+            fake = self.fake(x_noisy, cond)
             loss_f = (w * (fake.float() - target.float()) ** 2).mean() / self.accum
             loss_f.backward()
             lf.append(loss_f.detach())
@@ -332,10 +392,10 @@ class TDMTrainStep:
             # 2. generator update
             if self.red_g is not None:
                 self.red_g.enable(last)
-            pred = self.student(x_gen)
+            pred = self.student(x_gen, cond)
             with torch.no_grad():
-                real = self.teacher(x_noisy)
-                fake_g = self.fake(x_noisy)
+                real = self.teacher_predict(x_noisy, cond)
+                fake_g = self.fake(x_noisy, cond)
                 revised = (pred.detach() + real - fake_g).float()
                 weighting = (pred.detach().float() - real.float()).abs().mean(
                     dim=tuple(range(1, pred.dim())), keepdim=True).clamp(max=5.0)
