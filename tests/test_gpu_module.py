@@ -160,11 +160,11 @@ def test_fused_sampling_and_pool_launches_match_separate_launches(variant, D):
 
 @pytest.mark.parametrize("variant,D,B,H,strided", [("cog", 64, 1, 3, False), ("cog", 64, 2, 2, True),
                                                      ("wan", 128, 1, 2, False), ("wan", 128, 2, 1, True)])
-def test_inloop_pooled_pass_matches_pool_kv_at_full_length(variant, D, B, H, strided):
-    """At the real sequence lengths the pooled K/V pass runs INSIDE the score kernel's loop (one
-    source row per thread and K tile, vb_predict.hip kPoolIn): pooled K/V and the Gilbert-order
-    copies must equal the stand-alone vb_pool_kv bit for bit, and the mask must equal the predictor
-    run without the pass. Batched and on the processors' strided [B,L,H,D].transpose(1,2) views."""
+def test_fused_pooled_pass_matches_pool_kv_at_full_length(variant, D, B, H, strided):
+    """At the real sequence lengths, the pooled K/V pass run by the extra workgroups of the score
+    kernel's launch: pooled K/V and the Gilbert-order copies must equal the stand-alone
+    vb_pool_kv bit for bit, and the mask and scores must equal the predictor run without the pass.
+    Batched and on the processors' strided [B,L,H,D].transpose(1,2) views."""
     import vblade
     from vblade import ops
     m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)

@@ -30,38 +30,6 @@ constexpr int kMaxNb = 320;        // sampled blocks per side (L <= 40960 at blo
 // keys per LDS tile: D=64 streams four 32-key sampled blocks per barrier (16 MFMAs per wave),
 // D=128 two (also 16 MFMAs); a 3-deep ring keeps the LDS at 48 KiB (3 workgroups per CU)
 template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
-
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-// buffer descriptor words of an srd_t (raw buffer, stride 0, as make_buffer_rsrc builds it)
-__device__ __forceinline__ i32x4 srd_words(const srd_t& r) {
-  const uint64_t a = reinterpret_cast<uint64_t>(r.base);
-  return i32x4{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xFFFF), r.bytes, 0x00020000};
-}
-// vector-memory loads the compiler does not track (no s_waitcnt of its own): the caller waits with
-// a counted VB_WAIT_VMCNT and then calls pool_ready on the destinations before any use
-__device__ __forceinline__ u32x4 asm_load_b128(const i32x4& d, int voff) {
-  u32x4 x;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(x) : "v"(voff), "s"(d) : "memory");
-  return x;
-}
-__device__ __forceinline__ int asm_load_b32(const i32x4& d, int voff) {
-  int x;
-  asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(x) : "v"(voff), "s"(d) : "memory");
-  return x;
-}
-__device__ __forceinline__ void pool_ready(u32x4& a, u32x4& b, int& c) {
-  asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
-}
-
-// f(integral_constant<0>) ... f(integral_constant<N-1>), in order
-template <int N, int I = 0, class F>
-__device__ __forceinline__ void unroll_bodies(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    unroll_bodies<N, I + 1>(f);
-  }
-}
 #ifndef VB_PRED_BUFS
 #define VB_PRED_BUFS 3
 #endif
@@ -78,11 +46,9 @@ template <int D> constexpr int kPBufs = VB_PRED_BUFS;
 #ifndef VB_PRED_GATHER
 #define VB_PRED_GATHER 1   // K rows gathered by the score kernel's DMA (no sampled-row copy)
 #endif
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 #ifndef VB_FUSED_POOL_LAST
 #define VB_FUSED_POOL_LAST 0   // 1: pooling workgroups after the score workgroups (measured 1-4 % slower)
-#endif
-#ifndef VB_PRED_POOL_INLOOP
-#define VB_PRED_POOL_INLOOP 1   // the pooled K/V pass inside the score loop when it fits (else pooling WGs)
 #endif
 #ifndef VB_FUSED_POOL_WGS
 #define VB_FUSED_POOL_WGS 512   // workgroups of the predictor's launch that run the pooled K/V pass
@@ -99,7 +65,6 @@ struct PredParams {
   const float* rand_q; const float* rand_k;   // [B,H,block] uniforms (nullable): offsets drawn here
   PoolTask pool;                    // pooled K/V pass run by the first n_pool workgroups (fused launch)
   int n_pool;
-  int pool_items;                   // in-loop pooled pass: items (16-byte chunks of pooled rows) per thread
   int B, H, L, D, block, nb;
   float c;             // fp32(scale) * fp32(1.44269504), as the Triton kernel forms qk_scale
   float thr;
@@ -310,12 +275,7 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
   }
 }
 
-// kPoolIn: the pooled K/V pass run INSIDE the score loop by the score workgroups themselves (1:
-// pooled rows only; 2: also the Gilbert-order copies), one source row per thread and K tile, its
-// loads issued two tiles ahead like the K tiles: the HBM stream runs in the shadow of the MFMAs and
-// no workgroup slot (nor the launch's LDS) is spent on it. 0: no pass, or the pass run by the first
-// n_pool workgroups of the launch (pool_kv_span) when the in-loop form does not fit.
-template <int D, class T, bool kEnergy, int kPoolIn>
+template <int D, class T, bool kEnergy>
 __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel(const PredParams p) {
   constexpr int KS = D / 16;
   constexpr int kRowB = D * 2;                        // bytes per key row
@@ -456,104 +416,6 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
     const int sw = (D == 64) ? ((l32 >> 1) & 7) : (l32 & 15);
     k_lane[ks] = l32 * kRowB + 16 * ((2 * ks + half) ^ sw);
   }
-#if VB_PRED_GATHER
-  // ---- in-loop pooled K/V pass (kPoolIn > 0) -------------------------------------------------------
-  // Items of head bh: (pooled row pr, 16-byte chunk ch), Lp * kPCh of them; thread `tid` of this
-  // head's q-group qg owns items it0 + k * stride (k < pool_items), it0 = qg * 256 + tid, stride =
-  // nqg * 256 (a multiple of kPCh, so the chunk is fixed per lane). Step s of the pass (row r of
-  // item k, s = k * gap + r) runs at K tile s: its source-row index is loaded in body s - 3, its K
-  // and V chunks in body s - 2, and body s adds them (sequential fp32 sums, as pool_kv_span) and
-  // stores the copies / the finished pooled row. Every body issues the same number of pool loads
-  // and stores (inactive ones at an out-of-range offset: dropped), so the vmcnt counts stay
-  // constants. Placement of the work never changes a value: bit-identical to pool_kv_kernel.
-  constexpr int kPCh = D / 8;
-  constexpr int kPS = kPoolIn == 2 ? 4 : kPoolIn ? 2 : 0;      // pool stores per body
-  constexpr int kOOB = 0x7FFFFF00;                             // past every descriptor's extent
-  const int gap = p.pool.gap, Lp = p.pool.Lp;
-  const int n_it = kPoolIn ? p.pool_items : 0;
-  const int pch = threadIdx.x % kPCh;
-  const int pr0 = ((lin % nqg) * kPThreads + (int)threadIdx.x) / kPCh;
-  const int prs = nqg * kPThreads / kPCh;
-  srd_t rows_srd{}, vsrd{}, kpsrd{}, vpsrd{}, krsrd{}, vrsrd{};
-  int kstride_b = 0, vstride_b = 0;
-  if constexpr (kPoolIn > 0) {
-    const int b = bh / p.H, h = bh % p.H;
-    rows_srd = make_srd(p.rows ? (const void*)p.rows : p.q, p.rows ? p.L * 4 : 0);
-    const uint8_t* vslice = p.pool.v + 2 * (b * p.pool.vs[0] + h * p.pool.vs[1]);
-    vsrd = make_srd(vslice, (int)((int64_t)(p.L - 1) * p.pool.vs[2] * 2 + kRowB));
-    kpsrd = make_srd(p.pool.kp + (int64_t)bh * Lp * D * 2, Lp * D * 2);
-    vpsrd = make_srd(p.pool.vp + (int64_t)bh * Lp * D * 2, Lp * D * 2);
-    if constexpr (kPoolIn == 2) {
-      krsrd = make_srd(p.pool.k_r + (int64_t)bh * p.L * D * 2, p.L * D * 2);
-      vrsrd = make_srd(p.pool.v_r + (int64_t)bh * p.L * D * 2, p.L * D * 2);
-    }
-    kstride_b = (int)(p.ks[2] * 2);
-    vstride_b = (int)(p.pool.vs[2] * 2);
-  }
-  auto rsrc = [](const srd_t& r) __attribute__((always_inline)) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(r.base), (short)0, r.bytes, 0x00020000);
-  };
-  // The pool loads are inline asm, invisible to hipcc's waitcnt pass: with the bodies' guards it
-  // could not track them across the unrolled iterations and drained them a tile early. Their
-  // completion is covered by the bodies' own counted waits; `pool_ready` pins the uses behind them.
-  const i32x4 rows_d = srd_words(rows_srd), k_d = srd_words(ksrd), v_d = srd_words(vsrd);
-  struct PStep { int r, k; };   // wave-uniform: row within the item, item number
-  auto padv = [&](PStep& s) __attribute__((always_inline)) {
-    if (++s.r == gap) { s.r = 0; ++s.k; }
-  };
-  // source-row index of a step (rows[pos] with replicate padding; without rows: pos itself)
-  auto pool_ri = [&](const PStep& s) __attribute__((always_inline)) -> int {
-    const int pr = pr0 + s.k * prs;
-    const int pos = min(pr * gap + s.r, p.L - 1);
-    const bool ok = s.k < n_it && pr < Lp;
-    return asm_load_b32(rows_d, ok ? 4 * pos : kOOB);
-  };
-  auto pool_ld = [&](const PStep& s, int ri, u32x4& xk, u32x4& xv) __attribute__((always_inline)) {
-    const int pr = pr0 + s.k * prs;
-    const int pos = min(pr * gap + s.r, p.L - 1);
-    const bool ok = s.k < n_it && pr < Lp;
-    const int src = p.rows ? ri : pos;
-    xk = asm_load_b128(k_d, ok ? src * kstride_b + pch * 16 : kOOB);
-    xv = asm_load_b128(v_d, ok ? src * vstride_b + pch * 16 : kOOB);
-  };
-  float pacc_k[8], pacc_v[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) pacc_k[e] = pacc_v[e] = 0.f;
-  auto pool_use = [&](const PStep& s, const u32x4& xk, const u32x4& xv) __attribute__((always_inline)) {
-    const int pr = pr0 + s.k * prs;
-    const bool ok = s.k < n_it && pr < Lp;
-    const int g = pr * gap + s.r;
-    const bool first = s.r == 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      pacc_k[2 * e] = (first ? 0.f : pacc_k[2 * e]) + T::bits_to_f32(xk[e] & 0xffff);
-      pacc_k[2 * e + 1] = (first ? 0.f : pacc_k[2 * e + 1]) + T::bits_to_f32(xk[e] >> 16);
-      pacc_v[2 * e] = (first ? 0.f : pacc_v[2 * e]) + T::bits_to_f32(xv[e] & 0xffff);
-      pacc_v[2 * e + 1] = (first ? 0.f : pacc_v[2 * e + 1]) + T::bits_to_f32(xv[e] >> 16);
-    }
-    if constexpr (kPoolIn == 2) {   // the Gilbert-order copies (reordered row g < L)
-      const int o = (ok && g < p.L) ? (g * D + pch * 8) * 2 : kOOB;
-      __builtin_amdgcn_raw_buffer_store_b128(xk, rsrc(krsrd), o, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(xv, rsrc(vrsrd), o, 0, 0);
-    }
-    const bool last = s.r == gap - 1;
-    const float f = 1.0f / (float)gap;   // mean = sum * (1/N), as pool_kv_span
-    u32x4 ok4, ov4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      ok4[e] = pack2<T>(pacc_k[2 * e] * f, pacc_k[2 * e + 1] * f);
-      ov4[e] = pack2<T>(pacc_v[2 * e] * f, pacc_v[2 * e + 1] * f);
-    }
-    const int o = (ok && last) ? (pr * D + pch * 8) * 2 : kOOB;
-    __builtin_amdgcn_raw_buffer_store_b128(ok4, rsrc(kpsrd), o, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(ov4, rsrc(vpsrd), o, 0, 0);
-  };
-  PStep s_ri{0, 0}, s_ld{0, 0}, s_use{0, 0};   // the three pipeline stages' steps
-  int ri[2] = {0, 0};                          // source-row indices of steps t+2 / t+3 (set t & 1)
-  u32x4 pk[2] = {}, pv[2] = {};                // K/V chunks of steps t / t+1 (set t & 1)
-#else
-  constexpr int kPS = 0;
-#endif
   uint16_t* Rq = p.rbuf + ((int64_t)bh * nb + (wave_active ? qb : 0)) * nb * 32;   // this q-block
   const srd_t rsrd = make_srd(Rq, wave_active ? nb * 64 : 0);
 #if VB_PRED_GATHER
@@ -561,63 +423,29 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // issued, past the last tile too (offsets past the table read 0: row 0 into a slot no tile reads
   // any more), so the counts below are constant. Body t needs K(t) and I(t+2); younger than I(t+2)
   // are K(t+1) and S(t-1) (for t = 0: only K1), so K(t+1) stays in flight.
-  // With the in-loop pooled pass (kPoolIn): RI(s) = the source-row index load of pool step s,
-  // P(s) = its K/V chunk loads. Prologue: RI0 RI1 I0 I1 I2 | K0 P0 RI2 | K1 P1; body t issues
-  // RI(t+3) I(t+3) K(t+2), adds P(t), issues P(t+2) — so a body's wait for K(t) and I(t+2) also
-  // covers P(t) and RI(t+2) (both older).
   if (ntiles > 0) {
-    if constexpr (kPoolIn > 0) {
-      ri[0] = pool_ri(s_ri); padv(s_ri);
-      ri[1] = pool_ri(s_ri); padv(s_ri);
-      asm volatile("" ::: "memory");
-    }
     issue_idx(0);
     issue_idx(1);
     issue_idx(2);
     VB_WAIT_VMCNT(2);
     asm volatile("" ::: "memory");   // the offsets' LDS reads stay behind the wait
     issue(0);
-    if constexpr (kPoolIn > 0) {
-      asm volatile("" ::: "memory");
-      pool_ready(pk[0], pv[0], ri[0]);
-      pool_ready(pk[1], pv[1], ri[1]);
-      pool_ld(s_ld, ri[0], pk[0], pv[0]); padv(s_ld);
-      ri[0] = pool_ri(s_ri); padv(s_ri);
-      asm volatile("" ::: "memory");
-    }
-    VB_WAIT_VMCNT(1 + kInstPerWave + (kPoolIn > 0 ? 3 : 0));
+    VB_WAIT_VMCNT(1 + kInstPerWave);
     asm volatile("" ::: "memory");
     issue(1);
-    if constexpr (kPoolIn > 0) {
-      asm volatile("" ::: "memory");
-      pool_ld(s_ld, ri[1], pk[1], pv[1]); padv(s_ld);
-      asm volatile("" ::: "memory");
-    }
   }
 #else
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
 #endif
-  auto body = [&](int t, auto U, auto V) __attribute__((always_inline)) {
+  auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
 #if VB_PRED_GATHER
-    constexpr int v = decltype(V)::value;   // pool register set: step t's chunks, step t+2's index
-    if (t == 0) VB_WAIT_VMCNT(kInstPerWave + (kPoolIn > 0 ? 2 : 0));
-    else VB_WAIT_VMCNT(kInstPerWave + kSt + (kPoolIn > 0 ? kPS + 2 : 0));
+    if (t == 0) VB_WAIT_VMCNT(kInstPerWave);
+    else VB_WAIT_VMCNT(kInstPerWave + kSt);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if constexpr (kPoolIn > 0) {
-      pool_ready(pk[v], pv[v], ri[v]);   // P(t) and RI(t+2) landed (the wait above)
-      ri[v ^ 1] = pool_ri(s_ri); padv(s_ri);
-      asm volatile("" ::: "memory");
-    }
     issue_idx(t + 3);
     issue(t + 2);
-    if constexpr (kPoolIn > 0) {
-      asm volatile("" ::: "memory");
-      pool_use(s_use, pk[v], pv[v]); padv(s_use);
-      pool_ld(s_ld, ri[v], pk[v], pv[v]); padv(s_ld);
-      asm volatile("" ::: "memory");
-    }
 #else
     // retire this wave's DMA of tile t, then the barrier makes every wave's part visible and
     // guarantees tile t-1's buffer is no longer being read. vmcnt counts the R stores too, in issue
@@ -691,15 +519,13 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
 #pragma unroll
     for (int pr = 0; pr < kSt; ++pr) store16(rsrd, (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
   };
-  // the body is instantiated per ring slot (LDS offsets are immediates) and, with the in-loop
-  // pooled pass, per pool register set (t & 1): six bodies per iteration
-  constexpr int kUnroll = kPoolIn > 0 ? 2 * kBufs : kBufs;
-  for (int t0 = 0; t0 < ntiles; t0 += kUnroll) {
-    unroll_bodies<kUnroll>([&](auto I) __attribute__((always_inline)) {
-      constexpr int i = decltype(I)::value;
-      if (i == 0 || t0 + i < ntiles)
-        body(t0 + i, std::integral_constant<int, i % kBufs>{}, std::integral_constant<int, i & 1>{});
-    });
+  for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
+    body(t0, std::integral_constant<int, 0>{});
+    if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
+    if constexpr (kBufs > 2)
+      if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2 % kBufs>{});
+    if constexpr (kBufs > 3)
+      if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
   }
   static_assert(kBufs >= 2 && kBufs <= 4, "the loop body is instantiated once per ring slot");
 #if VB_PRED_GATHER
@@ -811,34 +637,10 @@ static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
   return predict_rows_bytes(B, H, L, D) + (uint64_t)B * H * nb * nb * 32 * 2;
 }
 
-// Can the pooled K/V pass run inside the score loop (kPoolIn)? Every thread of a head's nqg score
-// workgroups takes ceil(items / threads) items of `gap` steps, one step per K tile.
-static int pool_items_inloop(const PredParams& p) {
-  if (!VB_PRED_GATHER || !VB_PRED_POOL_INLOOP) return 0;
-  const int kt = (p.D == 64 ? kKeysPerTile<64> : kKeysPerTile<128>) / 32;
-  const int ntiles = (p.nb + kt - 1) / kt;
-  const int64_t threads = (int64_t)((p.nb + kPWaves - 1) / kPWaves) * kPThreads;
-  const int64_t items = (int64_t)p.pool.Lp * (p.D / 8);
-  const int64_t n_it = (items + threads - 1) / threads;
-  return n_it * p.pool.gap <= ntiles ? (int)n_it : 0;
-}
-
-template <int D, class T, int kPoolIn>
-static int launch_predict_mode(const PredParams& p, hipStream_t stream) {
-  const size_t smem = predict_smem_bytes(p.nb, D);
-  auto kern = mask_predict_kernel<D, T, !VB_PRED_SPLIT_ENERGY, kPoolIn>;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)smem) != hipSuccess)
-    return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
-  const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H + p.n_pool);
-  hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
-  return check_launch("mask_predict_kernel");
-}
-
 template <int D, class T>
 static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t staged) {
   const size_t smem = predict_smem_bytes(p.nb, D);
-  auto kern = mask_predict_kernel<D, T, !VB_PRED_SPLIT_ENERGY, 0>;
+  auto kern = mask_predict_kernel<D, T, !VB_PRED_SPLIT_ENERGY>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)smem) != hipSuccess)
     return fail(VB_ERR_LAUNCH, "mask_predict: cannot reserve LDS");
@@ -846,10 +648,6 @@ static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t st
                      0, stream, p);
   if (int rc = check_launch("sample_rows_kernel")) return rc;
   if (staged && hipEventRecord(staged, stream) != hipSuccess) return fail(VB_ERR_LAUNCH, "vb_mask_predict: hipEventRecord failed");
-  if (p.pool_items > 0) {   // the pooled K/V pass inside the score loop (no pooling workgroups)
-    if (VB_PRED_SPLIT_ENERGY) return fail(VB_ERR_UNSUPPORTED, "mask_predict: split energy build");
-    return p.pool.k_r ? launch_predict_mode<D, T, 2>(p, stream) : launch_predict_mode<D, T, 1>(p, stream);
-  }
   const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H + p.n_pool);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
   if (int rc = check_launch("mask_predict_kernel")) return rc;
@@ -918,15 +716,10 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
     t.Lp = (a->L + a->pool_gap - 1) / a->pool_gap;
     t.kp = reinterpret_cast<uint8_t*>(a->pool_kp); t.vp = reinterpret_cast<uint8_t*>(a->pool_vp);
     t.k_r = reinterpret_cast<uint8_t*>(a->pool_k_r); t.v_r = reinterpret_cast<uint8_t*>(a->pool_v_r);
-    if ((int64_t)(a->L - 1) * a->pool_v_stride[2] * 2 + 2 * a->D >= (int64_t(1) << 31))
-      return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: a v (b,h) slice spans >= 2 GiB");
-    p.pool_items = pool_items_inloop(p);
-    if (p.pool_items == 0) {   // pooling workgroups at the head of the launch instead
-      const int64_t items = (int64_t)a->B * a->H * t.Lp * (a->D / 8);
-      int n = (int)((items + 255) / 256);
-      n = n < kFusedPoolWgs ? n : kFusedPoolWgs;
-      p.n_pool = (n + 7) / 8 * 8;   // keeps blockIdx % 8 of the score workgroups (their XCD)
-    }
+    const int64_t items = (int64_t)a->B * a->H * t.Lp * (a->D / 8);
+    int n = (int)((items + 255) / 256);
+    n = n < kFusedPoolWgs ? n : kFusedPoolWgs;
+    p.n_pool = (n + 7) / 8 * 8;   // keeps blockIdx % 8 of the score workgroups (their XCD)
   }
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);
