@@ -421,21 +421,25 @@ def joint_from_branches(fwd: dict, log_gap: float) -> torch.Tensor:
 
 
 def bf16_ulp_distance(got: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
-    """Checker utility: distance in bf16 units in the last place between got and ref, both
-    rounded to bf16 (round to nearest even), counted on the monotone integer image of the bit
-    patterns (so it is exact across binades and signs). int64 tensor of got's shape."""
-    def ordered(x):
-        b = x.to(torch.bfloat16).view(torch.int16).to(torch.int64)
-        return torch.where(b < 0, -(b & 0x7FFF), b)
-    return (ordered(got.float()) - ordered(ref.float())).abs()
+    """Checker utility: |bf16(got) - bf16(ref)| in bf16 units in the last place at the reference's
+    magnitude, with magnitudes below the tensor's RMS binade measured in that binade's ULP (an
+    output near zero from cancellation is judged at the scale of the tensor, not in ULPs of its
+    own tiny value). bf16 keeps 8 significant bits: ULP(x) = 2^(floor(log2|x|) - 7). int64."""
+    g = got.float().to(torch.bfloat16).double()
+    r = ref.float().to(torch.bfloat16).double()
+    rms = float(r.pow(2).mean().sqrt())
+    floor = 2.0 ** math.floor(math.log2(rms)) if rms > 0 else 2.0 ** -126
+    mag = torch.clamp(r.abs(), min=floor)
+    ulp = torch.exp2(torch.floor(torch.log2(mag)) - 7)
+    return torch.round((g - r).abs() / ulp).to(torch.int64)
 
 
 ULP_BUCKETS = ((0, 0), (1, 1), (2, 2), (3, 4), (5, 8), (9, 16), (17, None))
 
 
 def bf16_ulp_histogram(got: torch.Tensor, ref: torch.Tensor) -> dict:
-    """Fractions of elements per bf16-ULP distance bucket (0, 1, 2, 3-4, 5-8, 9-16, >16), plus
-    the maximum distance (SURVEY §8d Quality)."""
+    """Fractions of elements per bf16-ULP distance bucket (0, 1, 2, 3-4, 5-8, 9-16, >16; see
+    bf16_ulp_distance), plus the maximum distance (SURVEY §8d Quality)."""
     d = bf16_ulp_distance(got, ref).flatten()
     n = d.numel()
     hist = {}
@@ -443,7 +447,8 @@ def bf16_ulp_histogram(got: torch.Tensor, ref: torch.Tensor) -> dict:
         sel = (d >= lo) if hi is None else ((d >= lo) & (d <= hi))
         key = f">{lo - 1}" if hi is None else (str(lo) if lo == hi else f"{lo}-{hi}")
         hist[key] = round(int(sel.sum()) / n, 6)
-    return {"ulp_hist": hist, "max_ulp": int(d.max()), "n": n}
+    return {"ulp_hist": hist, "max_ulp": int(d.max()), "n": n,
+            "ulp_unit": "bf16 ULP at |ref|, floored at the RMS binade of ref"}
 
 
 def adaptive_attention_bwd(q, k, v, dout, cfg: AdaptiveConfig, fwd: dict):

@@ -19,8 +19,12 @@ struct PoolTask {
 
 // Work items idx0, idx0 + step, ...: one 16-byte chunk of one pooled row each. Every reordered row
 // is read by exactly one item, which also writes it to the copies. The gap rows are read in groups
-// of 8 with every load of a group issued before any is used (16 loads in flight per thread: the
-// pass is HBM-latency bound otherwise); the fp32 sums keep the sequential row order.
+// of VB_POOL_GROUP with every load of a group issued before any is used (2 * VB_POOL_GROUP loads in
+// flight per thread: the pass is HBM-latency bound otherwise); the fp32 sums keep the sequential
+// row order.
+#ifndef VB_POOL_GROUP
+#define VB_POOL_GROUP 8
+#endif
 template <class T>
 __device__ __forceinline__ void pool_kv_span(const PoolTask& t, int64_t idx0, int64_t step) {
   const int CH = t.D / 8;
@@ -36,10 +40,11 @@ __device__ __forceinline__ void pool_kv_span(const PoolTask& t, int64_t idx0, in
     float ak[8], av[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) ak[e] = av[e] = 0.f;
-    for (int g0 = 0; g0 < t.gap; g0 += 8) {
-      u32x4 xk[8], xv[8];
+    constexpr int G = VB_POOL_GROUP;
+    for (int g0 = 0; g0 < t.gap; g0 += G) {
+      u32x4 xk[G], xv[G];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < G; ++u) {
         const int g = pr * t.gap + min(g0 + u, t.gap - 1);
         int pos = min(g, t.L - 1);   // replicate padding
         if (t.rows) pos = t.rows[pos];
@@ -47,7 +52,7 @@ __device__ __forceinline__ void pool_kv_span(const PoolTask& t, int64_t idx0, in
         xv[u] = *reinterpret_cast<const u32x4*>(vb + 2 * (int64_t)pos * t.vs[2]);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < G; ++u) {
         if (g0 + u >= t.gap) break;
         const int g = pr * t.gap + g0 + u;
         if (t.k_r && g < t.L) {
