@@ -329,6 +329,20 @@ def run(args):
             result["points"] = [measure_point(v, d, dev, dense_cache)
                                 for v, d in (("wan", None), ("cog-ml", None), ("cog", 0.05),
                                              ("cog", 0.3), ("cog", 0.5), ("cog", 0.7))]
+            if not args.no_pmc:
+                # counter-measured HBM-side traffic of the attention kernel at the Wan point and at
+                # the high-sparsity point (density 0.05), as GB/s against the 8 TB/s peak
+                for pt in result["points"]:
+                    if (pt["variant"], pt["mask"]) in (("wan", "energy rule"), ("cog", "density 0.05")):
+                        d = None if pt["mask"] == "energy rule" else 0.05
+                        tr = pmc_traffic(pt["variant"], density=d)
+                        if tr is not None:
+                            gbs = tr["bytes"] / (pt["attn_fwd_ms"] * 1e-3) / 1e9
+                            pt["traffic"] = tr["bytes"]
+                            pt["traffic_over_algorithmic"] = round(tr["bytes"] / pt["algorithmic_bytes"], 3)
+                            pt["hbm_gbs_counters"] = round(gbs, 1)
+                            pt["hbm_frac_counters"] = round(gbs / PEAK_HBM_GBS, 4)
+                            pt["traffic_detail"] = tr
             result["backward"] = measure_backward("cog", dev)
         if world == 1 and not args.no_cpu_baseline:
             base = "cog" if args.variant == "cog-ml" else args.variant
@@ -594,7 +608,7 @@ def quality_vs_oracle(mod, qkv, variant):
                                    "ulp_hist": h_re["ulp_hist"], "max_ulp": h_re["max_ulp"]}}
 
 
-def pmc_traffic(variant, timeout=300):
+def pmc_traffic(variant, timeout=300, density=None):
     """HBM-side bytes per attn_fwd_kernel launch from rocprofv3 PMC counters, one counter per
     pass (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
     tallies wide coalesced reads at half their bytes, so traffic = 2*FETCH + WRITE. The target
@@ -607,7 +621,8 @@ def pmc_traffic(variant, timeout=300):
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="vb_pmc_", dir="/tmp")
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
-               sys.executable, os.path.join(ROOT, "tools", "attn_only.py"), variant, "3", "attn"]
+               sys.executable, os.path.join(ROOT, "tools", "attn_only.py"), variant, "3", "attn",
+               "none" if density is None else str(density)]
         try:
             subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, check=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)

@@ -149,6 +149,10 @@ typedef struct vb_predict_args {
   int pool_gap;
   void* pool_kp; void* pool_vp;
   void* pool_k_r; void* pool_v_r;
+  /* pyr_k/pyr_v: the multi-level path's KV pyramid pass of vb_kv_pyramid (this call's k and
+   * pool_v, same rows; [B,H,vb_kv_pyramid_rows(L),D] each) run by extra workgroups of the score
+   * kernel's launch, like pool_* (which it excludes): no second stream and no events. */
+  void* pyr_k; void* pyr_v;
 } vb_predict_args;
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);

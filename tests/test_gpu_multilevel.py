@@ -86,6 +86,31 @@ def test_kv_pyramid_bit_exact(L, D, dtype):
         assert got[3].shape[2] == Lpad // 8
 
 
+@pytest.mark.parametrize("L,D,B,H,strided", [(17776, 64, 1, 3, False), (17776, 64, 2, 2, True),
+                                             (1000, 128, 1, 2, False), (32760, 128, 1, 2, True)])
+def test_kv_pyramid_in_the_predictor_launch_equals_standalone(L, D, B, H, strided):
+    """The pyramid pass run by extra workgroups of the score kernel's launch (ops.mask_predict
+    pyr=..., the module's inference path) writes the same pyramids, bit for bit, as vb_kv_pyramid,
+    and leaves the scores unchanged; batched and on strided [B,L,H,D].transpose(1,2) views."""
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(12)
+    shape = (B, L, H, D) if strided else (B, H, L, D)
+    q, k, v = (torch.randn(*shape, generator=g, device=DEV).bfloat16() for _ in range(3))
+    if strided:
+        q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    rows = torch.randperm(L, generator=torch.Generator().manual_seed(4)).int().to(DEV)
+    rq = torch.rand(B, H, 1, 128, device=DEV, generator=g)
+    rk = torch.rand(B, H, 1, 128, device=DEV, generator=g)
+    outs = ops.kv_pyramid_outputs(k)
+    po_p, _ = ops.mask_predict(q, k, rows=rows, want_mask=False, rand=(rq, rk), pyr=(v, outs))
+    po_r, _ = ops.mask_predict(q, k, rows=rows, want_mask=False, rand=(rq, rk))
+    ref = ops.kv_pyramid(k, v, rows)
+    torch.cuda.synchronize()
+    assert torch.equal(po_p, po_r)
+    for a, b in zip(outs, ref):
+        assert torch.equal(a, b)
+
+
 # ------------------------------------------------------------------------------------- level mask
 @pytest.mark.parametrize("case", ["m139", "m256", "m21", "m5"])
 def test_level_mask_kernel_on_reference_goldens(case):

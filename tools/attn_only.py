@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Run only the fused attention kernel (and optionally the predictor) N times on CogVideoX / Wan
-shapes — a target for rocprofv3 counter collection."""
+shapes — a target for rocprofv3 counter collection.
+usage: attn_only.py [cog|wan|cog-ml] [N] [attn|pred|all] [density (fixed kept fraction; default:
+the energy rule)]"""
 import os
 import sys
 
@@ -32,7 +34,9 @@ if variant == "cog-ml":   # the multi-level sampler path
         torch.cuda.synchronize()
     print("done")
     sys.exit(0)
-m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+density = float(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] != "none" else None
+over = {} if density is None else dict(min_retain_ratio=density, max_retain_ratio=density)
+m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **over)
 L = m.gilbert_rearranger.seq_len
 dev = torch.device("cuda")
 with torch.no_grad():

@@ -4,82 +4,15 @@
 // (_forward :1311-1320 builds k_2/k_4/k_8 with pad_to_multiple :1239-1250 and pooling :1252-1270)
 // and cogvideox/sample_evaluate/Triton/cogvideo_newattn.py transfer_attn_to_mask (:154-207).
 #include "vb_common.hpp"
+#include "vb_pyr.hpp"
 
 namespace vb {
 
 // ---- KV pyramid ---------------------------------------------------------------------------------
-// One thread = one 16-byte chunk (8 elements) of 8 consecutive reordered rows g0..g0+7, for K and
-// V: it reads the 8 rows once (replicate padding: rows >= L read row L-1) and writes 8 level-1
-// rows (zero beyond L), 4 level-2, 2 level-4 and 1 level-8 rows. Each level is the mean of the
-// previous level's pairs in fp32, rounded to the storage dtype, as torch.mean on a bf16/fp16 view
-// does. Consecutive lanes take consecutive chunks of a row, so every row read/write is coalesced.
+// The stand-alone launch of kv_pyramid_span (vb_pyr.hpp), grid-strided (pool_grid).
 template <int D, class T>
-__global__ void __launch_bounds__(256) kv_pyramid_kernel(const uint8_t* __restrict__ k, const uint8_t* __restrict__ v,
-                                                         int64_t ks0, int64_t ks1, int64_t ks2, int64_t vs0,
-                                                         int64_t vs1, int64_t vs2, const int32_t* __restrict__ rows,
-                                                         int B, int H, int L, int Lpad, uint8_t* __restrict__ kpyr,
-                                                         uint8_t* __restrict__ vpyr) {
-  constexpr int kCh = D / 8;   // 16-byte chunks per row
-  const int ngroups = Lpad / 8;
-  const int64_t total = (int64_t)B * H * ngroups * kCh;
-  for (int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
-       tid += (int64_t)gridDim.x * blockDim.x) {   // grid-stride (pool_grid)
-  const int ch = (int)(tid % kCh);
-  const int64_t rest = tid / kCh;
-  const int g = (int)(rest % ngroups);
-  const int bh = (int)(rest / ngroups);
-  const int b = bh / H, h = bh % H;
-  const int R = 15 * (Lpad / 8);
-  const int off2 = Lpad, off4 = Lpad + Lpad / 2, off8 = off4 + Lpad / 4;
-
-#pragma unroll
-  for (int mat = 0; mat < 2; ++mat) {
-    const uint8_t* src = mat == 0 ? k : v;
-    const int64_t s0 = mat == 0 ? ks0 : vs0, s1 = mat == 0 ? ks1 : vs1, s2 = mat == 0 ? ks2 : vs2;
-    uint8_t* dst = (mat == 0 ? kpyr : vpyr) + ((int64_t)bh * R * D + ch * 8) * 2;
-    const uint8_t* base = src + (b * s0 + h * s1 + ch * 8) * 2;
-    u32x4 x[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      int row = min(g * 8 + r, L - 1);
-      if (rows) row = rows[row];
-      x[r] = *reinterpret_cast<const u32x4*>(base + (int64_t)row * s2 * 2);
-    }
-    // level 1 (zero beyond L: the reference kernel's masked loads of the tail block)
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      u32x4 w = x[r];
-      if (g * 8 + r >= L) w = u32x4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(dst + (int64_t)(g * 8 + r) * D * 2) = w;
-    }
-    // levels 2, 4, 8
-    float f[8][8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t u = x[r][e];
-        f[r][2 * e] = T::bits_to_f32((uint16_t)(u & 0xFFFF));
-        f[r][2 * e + 1] = T::bits_to_f32((uint16_t)(u >> 16));
-      }
-    int n = 8, lvl_off[3] = {off2, off4, off8};
-#pragma unroll
-    for (int lv = 0; lv < 3; ++lv) {
-      n >>= 1;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (r >= n) break;
-        u32x4 w;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[r][e] = round_to<T>((f[2 * r][e] + f[2 * r + 1][e]) * 0.5f);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = pack2<T>(f[r][2 * e], f[r][2 * e + 1]);
-        const int prow = lvl_off[lv] + g * n + r;
-        *reinterpret_cast<u32x4*>(dst + (int64_t)prow * D * 2) = w;
-      }
-    }
-  }
-  }
+__global__ void __launch_bounds__(256) kv_pyramid_kernel(const PyrTask t) {
+  kv_pyramid_span<D, T>(t, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 // ---- level mask ----------------------------------------------------------------------------------
@@ -146,13 +79,12 @@ extern "C" int vb_kv_pyramid(const void* k, const void* v, const int64_t* k_stri
   const int64_t total = (int64_t)B * H * (Lpad / 8) * (D / 8);
   const dim3 grid(pool_grid(total));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const uint8_t* kb = static_cast<const uint8_t*>(k);
-  const uint8_t* vb_ = static_cast<const uint8_t*>(v);
-  uint8_t* kp = static_cast<uint8_t*>(kpyr);
-  uint8_t* vp = static_cast<uint8_t*>(vpyr);
-#define VB_PYR(DD, TT)                                                                                          \
-  hipLaunchKernelGGL((kv_pyramid_kernel<DD, TT>), grid, dim3(256), 0, st, kb, vb_, k_stride[0], k_stride[1],   \
-                     k_stride[2], v_stride[0], v_stride[1], v_stride[2], rows, B, H, L, Lpad, kp, vp)
+  PyrTask t{};
+  t.k = static_cast<const uint8_t*>(k); t.v = static_cast<const uint8_t*>(v);
+  for (int i = 0; i < 3; ++i) { t.ks[i] = k_stride[i]; t.vs[i] = v_stride[i]; }
+  t.rows = rows; t.B = B; t.H = H; t.L = L; t.Lpad = Lpad;
+  t.kpyr = static_cast<uint8_t*>(kpyr); t.vpyr = static_cast<uint8_t*>(vpyr);
+#define VB_PYR(DD, TT) hipLaunchKernelGGL((kv_pyramid_kernel<DD, TT>), grid, dim3(256), 0, st, t)
   if (dtype == VB_DTYPE_BF16) {
     if (D == 64) VB_PYR(64, BF16); else VB_PYR(128, BF16);
   } else if (dtype == VB_DTYPE_F16) {

@@ -18,6 +18,7 @@
 
 #include "vb_tiles.hpp"
 #include "vb_pool.hpp"
+#include "vb_pyr.hpp"
 
 namespace vb {
 
@@ -64,7 +65,8 @@ struct PredParams {
   int32_t* q_off; int32_t* k_off;   // inputs, or outputs when rand_q/rand_k are given
   const float* rand_q; const float* rand_k;   // [B,H,block] uniforms (nullable): offsets drawn here
   PoolTask pool;                    // pooled K/V pass run by the first n_pool workgroups (fused launch)
-  int n_pool;
+  PyrTask pyr;                      // or the multi-level KV pyramid pass (pool_kind 2)
+  int n_pool, pool_kind;
   int B, H, L, D, block, nb;
   float c;             // fp32(scale) * fp32(1.44269504), as the Triton kernel forms qk_scale
   float thr;
@@ -302,7 +304,9 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   const int wg = (int)blockIdx.x;
 #else
   if ((int)blockIdx.x < p.n_pool) {
-    pool_kv_span<T>(p.pool, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)p.n_pool * blockDim.x);
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)p.n_pool * blockDim.x;
+    if (p.pool_kind == 2) kv_pyramid_span<D, T>(p.pyr, i0, st);
+    else pool_kv_span<T>(p.pool, i0, st);
     return;
   }
   const int wg = (int)blockIdx.x - p.n_pool;
@@ -720,6 +724,25 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
     int n = (int)((items + 255) / 256);
     n = n < kFusedPoolWgs ? n : kFusedPoolWgs;
     p.n_pool = (n + 7) / 8 * 8;   // keeps blockIdx % 8 of the score workgroups (their XCD)
+  }
+  if (a->pyr_k) {   // the KV pyramid pass rides in the score kernel's launch
+    if (a->pool_kp) return fail(VB_ERR_INVALID, "vb_mask_predict: pool_* and pyr_* are exclusive");
+    if (!a->pyr_v || !a->pool_v) return fail(VB_ERR_INVALID, "vb_mask_predict: pyr_k needs pyr_v and pool_v");
+    for (int i = 0; i < 3; ++i)
+      if (a->pool_v_stride[i] & 7) return fail(VB_ERR_INVALID, "vb_mask_predict: pool_v strides must be multiples of 8");
+    if (((reinterpret_cast<uintptr_t>(a->k) | reinterpret_cast<uintptr_t>(a->pool_v) |
+          reinterpret_cast<uintptr_t>(a->pyr_k) | reinterpret_cast<uintptr_t>(a->pyr_v)) & 15) != 0)
+      return fail(VB_ERR_INVALID, "vb_mask_predict: pyramid tensors must be 16-byte aligned");
+    PyrTask& t = p.pyr;
+    t.k = reinterpret_cast<const uint8_t*>(a->k); t.v = reinterpret_cast<const uint8_t*>(a->pool_v);
+    for (int i = 0; i < 3; ++i) { t.ks[i] = a->k_stride[i]; t.vs[i] = a->pool_v_stride[i]; }
+    t.rows = a->rows; t.B = a->B; t.H = a->H; t.L = a->L; t.Lpad = nb * 128;
+    t.kpyr = reinterpret_cast<uint8_t*>(a->pyr_k); t.vpyr = reinterpret_cast<uint8_t*>(a->pyr_v);
+    const int64_t items = (int64_t)a->B * a->H * (t.Lpad / 8) * (a->D / 8);
+    int n = (int)((items + 255) / 256);
+    n = n < kFusedPoolWgs ? n : kFusedPoolWgs;
+    p.n_pool = (n + 7) / 8 * 8;   // keeps blockIdx % 8 of the score workgroups (their XCD)
+    p.pool_kind = 2;
   }
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_PRED")) p.dbg = atoi(d);

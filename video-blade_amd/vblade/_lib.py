@@ -57,6 +57,7 @@ class PredictArgs(ctypes.Structure):
         ("rand_q", _vp), ("rand_k", _vp),
         ("pool_v", _vp), ("pool_v_stride", _i64x3), ("pool_gap", ctypes.c_int),
         ("pool_kp", _vp), ("pool_vp", _vp), ("pool_k_r", _vp), ("pool_v_r", _vp),
+        ("pyr_k", _vp), ("pyr_v", _vp),
     ]
 
 

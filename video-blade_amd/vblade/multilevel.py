@@ -14,10 +14,11 @@ cogvideox/sample_evaluate/modify_cogvideo.py:9):
     [B,H,nb,nb] int level mask (0 skip, 1/2/4/8 = K/V mean-pooled by that factor, +ln p logit bias).
 
 Every tensor op runs in libvblade_hip.so:
-  1. vb_mask_predict (the rand draws ranked inside its sampling launch) — sampled pooled scores (Gilbert order through ``rows``)
+  1. vb_mask_predict (the rand draws ranked inside its sampling launch) — sampled pooled scores
+     (Gilbert order through ``rows``); the KV pyramid pass (one pass over K/V: reordered level-1
+     rows + 2x/4x/8x pooled rows, HBM-bound) runs as extra workgroups of the score kernel's launch
   2. vb_level_mask  — rank bands -> uint8 level mask
-  3. vb_kv_pyramid  — one pass over K/V: reordered level-1 rows + 2x/4x/8x pooled rows
-  4. vb_ml_attn_fwd — one softmax over every kept block's keys at its level; q rows gathered and
+  3. vb_ml_attn_fwd — one softmax over every kept block's keys at its level; q rows gathered and
                       out rows scattered through the Gilbert index inside the kernel
 """
 from __future__ import annotations
@@ -43,9 +44,10 @@ def density(mask_ratios=None) -> float:
     return sum((e - s) / v for v, (s, e) in r.items() if v != 0)
 
 
-def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=None, staged_event=None):
+def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=None, pyr=None):
     """efficient_attn_with_pooling + transfer_attn_to_mask on the (reordered through ``rows``)
-    q, k: returns (po [B,H,nb,nb] q.dtype, level mask uint8 [B,H,nb,nb])."""
+    q, k: returns (po [B,H,nb,nb] q.dtype, level mask uint8 [B,H,nb,nb]). ``pyr=(v, outs)``: the
+    KV pyramid pass in the score kernel's launch (ops.mask_predict)."""
     B, H, L, D = q.shape
     rand = None
     if q_off is None and k_off is None:
@@ -54,8 +56,7 @@ def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=N
         rand = (torch.rand(B, H, 1, BLOCK, device=q.device), torch.rand(B, H, 1, BLOCK, device=q.device))
     elif q_off is None or k_off is None:
         q_off, k_off = draw_sample_offsets_qk(B, H, q.device, BLOCK, 32)
-    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, staged_event=staged_event,
-                             rand=rand)
+    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, rand=rand, pyr=pyr)
     return po, ops.level_mask(po, mask_ratios)
 
 
@@ -122,6 +123,8 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
 
     def __init__(self, *, mask_ratios=None, ref_tail: bool = True, log_every: int = 600,
                  overlap: bool = True, **overrides):
+        """overlap: run the KV pyramid pass inside the predictor's launch (True) or as its own
+        launch after it."""
         super().__init__()
         cfg = dict(DEFAULTS)
         unknown = set(overrides) - set(cfg)
@@ -140,7 +143,6 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
         self.last_mask: Optional[torch.Tensor] = None
         self.attn_events: Optional[list] = None   # bench.py's live kernel timing (see attention.py)
         self.overlap = bool(overlap)
-        self._side = ops.SideStream()
 
     def _rows(self, device):
         if not self.use_rearrange:
@@ -171,19 +173,19 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
             self.sparsity_counter += 1
             return out
         with torch.no_grad():
-            # the pyramid pass (HBM-bound) on a side stream beside the predictor's score kernel
-            side = None
-            outs = ops.kv_pyramid_outputs(k)   # before the predictor's temporaries (see attention.py)
+            # the pyramid pass (HBM-bound) rides in the predictor's launch beside the MFMA-bound
+            # score workgroups (one stream, no events), or runs after it
+            outs = ops.kv_pyramid_outputs(k)   # before the predictor's temporaries
             if level_mask is None:
-                ev = self._side.event(q.device) if self.overlap else None
                 _, mask = predict_level_mask(q, k, rows=rows, mask_ratios=self.mask_ratios,
-                                             q_off=q_off, k_off=k_off, staged_event=ev)
-                side = self._side.fork(q.device, event=ev) if self.overlap else None
+                                             q_off=q_off, k_off=k_off,
+                                             pyr=(v, outs) if self.overlap else None)
             else:
                 mask = level_mask.to(torch.uint8).contiguous()
-            kpyr, vpyr = ops.kv_pyramid(k, v, rows, stream=side, out=outs)
-            if side is not None:
-                self._side.join(q.device)
+            if level_mask is None and self.overlap:
+                kpyr, vpyr = outs
+            else:
+                kpyr, vpyr = ops.kv_pyramid(k, v, rows, out=outs)
             ev = self.attn_events
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)

@@ -283,7 +283,7 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
 # ----------------------------------------------------------------------------------------------
 def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.95, min_keep=1,
                  max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True,
-                 staged_event=None, rand=None, pool=None):
+                 staged_event=None, rand=None, pool=None, pyr=None):
     """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
     po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb] (None with want_mask=False: the scores
     only, no energy rule). ``staged_event`` (a torch.cuda.Event) is recorded once the sampled
@@ -293,7 +293,9 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     q_off/k_off; the topk offsets are drawn inside the sampling launch.
     ``pool=(v, gap, outs)``: the pooled K/V pass (vb_pool_kv of k, v through ``rows``) run by extra
     workgroups of the score kernel's launch on the current stream; ``outs`` = pool_kv_outputs(k,
-    gap, reordered) receives kp, vp[, k_r, v_r]."""
+    gap, reordered) receives kp, vp[, k_r, v_r].
+    ``pyr=(v, outs)``: the multi-level KV pyramid pass (vb_kv_pyramid of k, v through ``rows``)
+    run the same way; ``outs`` = kv_pyramid_outputs(k). Excludes ``pool``."""
     if k.shape != q.shape:
         raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
                          f"got k {tuple(k.shape)}")
@@ -340,6 +342,18 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
         a.pool_kp, a.pool_vp = outs[0].data_ptr(), outs[1].data_ptr()
         if len(outs) > 2:
             a.pool_k_r, a.pool_v_r = outs[2].data_ptr(), outs[3].data_ptr()
+    if pyr is not None:
+        if pool is not None:
+            raise ValueError("mask_predict: pool and pyr are exclusive")
+        v, outs = pyr
+        v = _aligned_bhld(v)
+        if v.shape != k.shape:
+            raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
+                             f"got v {tuple(v.shape)}")
+        if outs[0].shape != (B, H, kv_pyramid_rows(L), D) or outs[1].shape != outs[0].shape:
+            raise ValueError("mask_predict: pyramid outputs must come from kv_pyramid_outputs(k)")
+        a.pool_v, a.pool_v_stride = v.data_ptr(), _s3(v)
+        a.pyr_k, a.pyr_v = outs[0].data_ptr(), outs[1].data_ptr()
     check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
 
@@ -569,47 +583,6 @@ def ml_attention_bwd(dout, q, kpyr, vpyr, level_mask_u8, out, lse, *, rows=None,
     a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
     check(lib.vb_ml_attn_bwd(ctypes.byref(a), _stream(dev)), "vb_ml_attn_bwd")
     return dq, dk, dv
-
-
-class SideStream:
-    """A second HIP stream per device for work that is independent within one call (the pooled
-    K/V pass beside the mask predictor). ``fork()`` makes it wait for the current stream;
-    ``join()`` makes the current stream wait for it."""
-
-    def __init__(self):
-        self._streams = {}
-        self._events = {}
-
-    def event(self, dev):
-        """A reusable HIP event (created and recorded once so its handle exists) that the
-        library records mid-call (vb_predict_args.staged_event)."""
-        key = torch.device(dev).index
-        ev = self._events.get(key)
-        if ev is None:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            self._events[key] = ev
-        return ev
-
-    def get(self, dev):
-        key = torch.device(dev).index
-        st = self._streams.get(key)
-        if st is None:
-            st = torch.cuda.Stream(device=dev)
-            self._streams[key] = st
-        return st
-
-    def fork(self, dev, event=None):
-        """The side stream, made to wait for the current stream (or for ``event`` only)."""
-        st = self.get(dev)
-        if event is not None:
-            st.wait_event(event)
-        else:
-            st.wait_stream(torch.cuda.current_stream(dev))
-        return st
-
-    def join(self, dev):
-        torch.cuda.current_stream(dev).wait_stream(self.get(dev))
 
 
 def default_scale(D: int) -> float:
