@@ -28,6 +28,7 @@ namespace vb {
 constexpr int kPWaves = VB_PRED_WAVES;
 constexpr int kPThreads = 64 * kPWaves;
 constexpr int kMaxNb = 320;        // sampled blocks per side (L <= 40960 at block 128)
+constexpr int kEnergyRow = kMaxNb + 16;   // LDS floats per energy-rule row buffer (keys padded to 16)
 // keys per LDS tile: D=64 streams four 32-key sampled blocks per barrier (16 MFMAs per wave),
 // D=128 two (also 16 MFMAs); a 3-deep ring keeps the LDS at 48 KiB (3 workgroups per CU)
 template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
@@ -98,11 +99,11 @@ __device__ __forceinline__ uint32_t storage_bits(float v) {
 }
 
 // Energy rule on one row of nc normalised scores held (storage-rounded, as f32) in LDS `val`
-// (room for kMaxNb + 4 floats); `keys` is LDS scratch for kMaxNb + 4 uint32. One full wave.
+// (room for kEnergyRow floats); `keys` is LDS scratch for kEnergyRow uint32. One full wave.
 // Sort key = (storage bits << 16) | (0xFFFF - index): larger value first, ties -> lower index
 // first (a stable descending sort), one unsigned compare per pair. The fp32-accumulated
 // cumulative sum over the sorted values runs sequentially (bit-identical to torch's CPU cumsum)
-// through v_readlane on a register-distributed copy, recording each prefix in its own lane.
+// as one uniform chain; lane t keeps the prefix at its own position where the clamp can see it.
 template <class T, int U>
 __device__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
                             int min_keep, int max_keep, int force_cols, bool force_all) {
@@ -116,15 +117,22 @@ __device__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int
     if (j < nc) keys[j] = mykey[u];
     rank[u] = 0;
   }
-  if (lane < 4) keys[nc + lane] = 0u;  // pad: never greater than a real key
+  const int nc16 = (nc + 15) & ~15;
+  if (nc + lane < nc16) keys[nc + lane] = 0u;  // pad to 16: never greater than a real key
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
-  for (int t4 = 0; t4 < nc; t4 += 4) {
-    const u32x4 kk = *reinterpret_cast<const u32x4*>(keys + t4);
+  // 16 keys (four 16-byte broadcasts) per step, two steps unrolled: eight LDS reads in flight
+#pragma unroll 2
+  for (int t16 = 0; t16 < nc16; t16 += 16) {
+    u32x4 kk[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+    for (int c = 0; c < 4; ++c) kk[c] = *reinterpret_cast<const u32x4*>(keys + t16 + 4 * c);
 #pragma unroll
-      for (int u = 0; u < U; ++u) rank[u] += (kk[e] > mykey[u]) ? 1 : 0;
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < U; ++u) rank[u] += (kk[c][e] > mykey[u]) ? 1 : 0;
   }
   // scatter values into sorted order (reuse `keys` as float storage after a wave barrier)
   __builtin_amdgcn_wave_barrier();
@@ -140,33 +148,52 @@ __device__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int
 #pragma unroll
   for (int u = 0; u < U; ++u)
     if (lane + 64 * u < nc) sorted[rank[u]] = vals[u];
+  if (nc + lane < nc16) sorted[nc + lane] = 0.f;
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
-  float sv[U], pre[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int t = lane + 64 * u;
-    sv[u] = (t < nc) ? sorted[t] : 0.f;
-    pre[u] = 0.f;
-  }
+  // fp32 sequential cumulative sum (torch's CPU cumsum) as ONE chain, identical in every lane,
+  // over the sorted values read by 16-byte LDS broadcasts. The clamped count k only depends on the
+  // first min(nc, max_keep) prefixes (cum is non-decreasing, k = #prefixes below the threshold,
+  // then clamped to max_keep), so lane t records the prefix at position t + 64u only there; the
+  // total is the chain's end.
+  const int need = min(nc, max_keep);
   float acc = 0.f;
+  float pre[U];
+  const float4* s4 = reinterpret_cast<const float4*>(sorted);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (64 * u >= nc) break;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      acc += __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(sv[u]), i));  // sv == 0 past nc
-      pre[u] = (lane == i) ? acc : pre[u];
+    pre[u] = 0.f;
+    if (64 * u >= nc16) break;
+    if (64 * u < need) {
+#pragma unroll 4
+      for (int i4 = 0; i4 < 16; ++i4) {
+        if (64 * u + 4 * i4 >= nc16) break;
+        const float4 w = s4[16 * u + i4];
+        const int i = 4 * i4;
+        acc += w.x; pre[u] = (lane == i) ? acc : pre[u];
+        acc += w.y; pre[u] = (lane == i + 1) ? acc : pre[u];
+        acc += w.z; pre[u] = (lane == i + 2) ? acc : pre[u];
+        acc += w.w; pre[u] = (lane == i + 3) ? acc : pre[u];
+      }
+    } else {
+#pragma unroll 4
+      for (int i4 = 0; i4 < 16; ++i4) {
+        if (64 * u + 4 * i4 >= nc16) break;
+        const float4 w = s4[16 * u + i4];
+        acc += w.x; acc += w.y; acc += w.z; acc += w.w;   // padding past nc adds zeros
+      }
     }
   }
-  const float total = round_to<T>(acc);     // cum_energy[..., -1]
+  const float total = round_to<T>(acc);   // cum_energy[..., -1]
   const float th = round_to<T>(total * thr);
   int k = 0;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int t = lane + 64 * u;
-    k += __popcll(__ballot(t < nc && round_to<T>(pre[u]) < th));
+    k += __popcll(__ballot(t < need && round_to<T>(pre[u]) < th));
   }
+  // all `need` prefixes below the threshold: the crossing is at or past need (k = need, which the
+  // clamp maps like the reference's first crossing / nc)
   k = min(max(k, min_keep), max_keep);
   int kept = 0;
 #pragma unroll
@@ -315,7 +342,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   const int nb = p.nb;
   float* mrow_s = reinterpret_cast<float*>(smem);
   uint8_t* ktile = smem + kPWaves * 32 * 4;
-  float* rowbuf = reinterpret_cast<float*>(ktile);  // [4][2][kMaxNb + 4], reused after the loop
+  float* rowbuf = reinterpret_cast<float*>(ktile);  // [4][2][kEnergyRow], reused after the loop
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -542,8 +569,8 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
 
   // Po[qb, j] = storage(max_r exp2(R[r][j] - m_r)) = storage(exp2(max_r (R[r][j] - m_r)))
   // (exp2 and the rounding are monotone), then the storage-dtype row normalisation
-  float* val = rowbuf + wave * 2 * (kMaxNb + 4);
-  uint32_t* keys = reinterpret_cast<uint32_t*>(val + kMaxNb + 4);
+  float* val = rowbuf + wave * 2 * (kEnergyRow);
+  uint32_t* keys = reinterpret_cast<uint32_t*>(val + kEnergyRow);
   const float* mw = mrow_s + wave * 32;
   // this wave's R columns were stored by its own lanes: wait for them and drop any stale L1 line
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
@@ -555,23 +582,34 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
     for (int e = 0; e < 4; ++e) mreg[r + e] = x[e];
   }
   float part = 0.f;
-  for (int j = lane; j < nb; j += 64) {
-    // the block's 32 row maxima: 64 contiguous bytes, four 16-byte loads in flight at once
-    u32x4 w[4];
+  // three columns per lane per pass (12 loads in flight; one pass up to nb = 192): the block's 32
+  // row maxima are 64 contiguous bytes
+  for (int j0 = 0; j0 < nb; j0 += 192) {
+    u32x4 w[3][4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) w[c] = reinterpret_cast<const u32x4*>(Rq + j * 32)[c];
-    float cm = -INFINITY;
+    for (int h = 0; h < 3; ++h) {
+      const int jj = min(j0 + 64 * h + lane, nb - 1);
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c) w[h][c] = reinterpret_cast<const u32x4*>(Rq + jj * 32)[c];
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 8 * c + 2 * e;
-        cm = max3f(cm, T::bits_to_f32((uint16_t)(w[c][e] & 0xFFFF)) - mreg[r],
-                   T::bits_to_f32((uint16_t)(w[c][e] >> 16)) - mreg[r + 1]);
+    for (int h = 0; h < 3; ++h) {
+      const int j = j0 + 64 * h + lane;
+      float cm = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 8 * c + 2 * e;
+          cm = max3f(cm, T::bits_to_f32((uint16_t)(w[h][c][e] & 0xFFFF)) - mreg[r],
+                     T::bits_to_f32((uint16_t)(w[h][c][e] >> 16)) - mreg[r + 1]);
+        }
+      cm = round_to<T>(exp2_fast(cm));
+      if (j < nb) {
+        val[j] = cm;
+        part += cm;
       }
-    cm = round_to<T>(exp2_fast(cm));
-    val[j] = cm;
-    part += cm;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
   const float tot = round_to<T>(part);
@@ -606,7 +644,7 @@ template <class T>
 __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int rows_total, int nc, float thr,
                                                           int min_keep, int max_keep, int force_tail, int nr,
                                                           uint8_t* mask, unsigned long long* count) {
-  __shared__ __attribute__((aligned(16))) float buf[4][2 * (kMaxNb + 4)];
+  __shared__ __attribute__((aligned(16))) float buf[4][2 * (kEnergyRow)];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows_total) return;
@@ -617,7 +655,7 @@ __global__ void __launch_bounds__(256) energy_mask_kernel(const void* po, int ro
   __builtin_amdgcn_wave_barrier();
   const int i = row % nr;
   const bool force_all = force_tail > 0 && i >= nr - force_tail;
-  const int kept = energy_row<T>(val, reinterpret_cast<uint32_t*>(val + kMaxNb + 4), mask + (int64_t)row * nc, nc,
+  const int kept = energy_row<T>(val, reinterpret_cast<uint32_t*>(val + kEnergyRow), mask + (int64_t)row * nc, nc,
                                  thr, min_keep, max_keep, force_tail, force_all);
   if (count && lane == 0) atomicAdd(count, (unsigned long long)kept);
 }
@@ -626,7 +664,7 @@ static size_t predict_smem_bytes(int nb, int D) {
   (void)nb;
   const size_t tiles = D == 64 ? (size_t)kPBufs<64> * kKeysPerTile<64> * 64 * 2
                                : (size_t)kPBufs<128> * kKeysPerTile<128> * 128 * 2;
-  const size_t scratch = (size_t)kPWaves * 2 * (kMaxNb + 4) * 4;
+  const size_t scratch = (size_t)kPWaves * 2 * (kEnergyRow) * 4;
   const size_t ring = VB_PRED_GATHER ? 4 * kPWaves * 256 : 0;   // gather mode: the row-offset ring
   return kPWaves * 32 * 4 + (tiles + ring > scratch ? tiles + ring : scratch);
 }
