@@ -71,8 +71,9 @@ def main():
     ap.add_argument("--variant", default="cog", choices=["cog", "wan"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--tdm", action="store_true",
-                    help="the two-model TDM step (student + fake-score model + frozen teacher, two AdamW, "
-                         "two reducers; train_cogvideo_tdm.py:1301-1325, 1640-1737)")
+                    help="the two-model TDM step (student + fake-score model with sparse attention, frozen "
+                         "dense teacher with CFG, two AdamW, two reducers; train_cogvideo_tdm.py:1301-1325, "
+                         "1640-1737)")
     ap.add_argument("--stub-cpu", action="store_true", help=argparse.SUPPRESS)  # launcher tests
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
@@ -102,10 +103,14 @@ def main():
                                  gradient_checkpointing=True, device=dev, seed=0)
     g = torch.Generator(device=dev).manual_seed(100 + rank)
     if args.tdm:
-        step = T.TDMTrainStep(model, lr=1e-4, lr_fake=1e-4, accum=args.accum, distributed=world > 1)
+        # teacher: a dense (unpatched) copy with classifier-free guidance, cfg 3.5 (train_tdm_1.sh)
+        step = T.TDMTrainStep(model, lr=1e-4, lr_fake=1e-4, accum=args.accum, distributed=world > 1,
+                              cfg=3.5)
         micro = [(torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16(),
                   torch.randn(args.batch, L, hidden, generator=g, device=dev).bfloat16(),
-                  torch.rand(args.batch, 1, 1, generator=g, device=dev) + 0.5) for _ in range(args.accum)]
+                  torch.rand(args.batch, 1, 1, generator=g, device=dev) + 0.5,
+                  (torch.randn(args.batch, 1, hidden, generator=g, device=dev) * 0.5).bfloat16())
+                 for _ in range(args.accum)]
     else:
         reducer = T.BucketedGradReducer(model.lora_parameters()) if world > 1 else None
         step = T.TrainStep(model, lr=1e-4, accum=args.accum, reducer=reducer)
@@ -140,7 +145,7 @@ def main():
         ms_step = 1000.0 * elapsed / args.steps
         samples = world * args.batch * args.accum * args.steps
         print(json.dumps({
-            "metric": ("TDM two-model step (student + fake-score + teacher)" if args.tdm else
+            "metric": ("TDM two-model step (student + fake-score, sparse; dense CFG teacher)" if args.tdm else
                        "TDM-style LoRA training step") + ", stand-in blocks with " +
                       ("CogVideoX-5B" if args.variant == "cog" else "Wan2.1-1.3B") + " attention geometry",
             "value": round(samples / elapsed, 4), "unit": "samples/s", "n_gpus": world,

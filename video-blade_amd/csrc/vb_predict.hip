@@ -41,6 +41,12 @@ template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
 #ifndef VB_PRED_SCHED
 #define VB_PRED_SCHED 4   // K-fragment reads issued this many MFMAs ahead (0: the compiler's order)
 #endif
+#ifndef VB_PRED_RCOLS
+#define VB_PRED_RCOLS 3   // R-readback columns per lane per pass in the epilogue
+#endif
+#ifndef VB_PRED_OCC
+#define VB_PRED_OCC   // e.g. __attribute__((amdgpu_waves_per_eu(4, 4))): a register budget for 4 waves/SIMD
+#endif
 #ifndef VB_PRED_MIN_WG
 #define VB_PRED_MIN_WG 2
 #endif
@@ -105,7 +111,7 @@ __device__ __forceinline__ uint32_t storage_bits(float v) {
 // cumulative sum over the sorted values runs sequentially (bit-identical to torch's CPU cumsum)
 // as one uniform chain; lane t keeps the prefix at its own position where the clamp can see it.
 template <class T, int U>
-__device__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
+__device__ __forceinline__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
                             int min_keep, int max_keep, int force_cols, bool force_all) {
   const int lane = threadIdx.x & 63;
   uint32_t mykey[U];
@@ -121,8 +127,8 @@ __device__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int
   if (nc + lane < nc16) keys[nc + lane] = 0u;  // pad to 16: never greater than a real key
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
-  // 16 keys (four 16-byte broadcasts) per step, two steps unrolled: eight LDS reads in flight
-#pragma unroll 2
+  // 16 keys (four 16-byte broadcasts) per step: four LDS reads in flight
+#pragma unroll 1
   for (int t16 = 0; t16 < nc16; t16 += 16) {
     u32x4 kk[4];
 #pragma unroll
@@ -210,7 +216,7 @@ __device__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int
 }
 // U = values per lane, the smallest that covers the row (ranks cost nc * U compares per lane)
 template <class T>
-__device__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
+__device__ __forceinline__ int energy_row(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
                           int min_keep, int max_keep, int force_cols, bool force_all) {
   switch ((nc + 63) >> 6) {
     case 1: return energy_row_u<T, 1>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols, force_all);
@@ -305,7 +311,7 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
 }
 
 template <int D, class T, bool kEnergy>
-__global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel(const PredParams p) {
+__global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_predict_kernel(const PredParams p) {
   constexpr int KS = D / 16;
   constexpr int kRowB = D * 2;                        // bytes per key row
   constexpr int kKT = kKeysPerTile<D> / 32;          // sampled key blocks per tile
@@ -381,7 +387,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // wave DMAs the offsets of its own rows into a small LDS ring two tiles ahead (one 4-byte lane
   // each, ordered so that lane L's four rows are 16 contiguous bytes), reads them back and issues
   // the row DMAs with per-lane voffsets. 27 MB of row copies per CogVideoX call are not made.
-  static_assert(kBufs == 3, "the gather pipeline's vmcnt counts assume a 3-slot K ring");
+  static_assert(kBufs == 2 || kBufs == 3, "the gather pipeline's vmcnt counts assume a 2- or 3-slot K ring");
   constexpr int kChunks = kRowB / 16;
   const uint8_t* kslice = reinterpret_cast<const uint8_t*>(p.k) + 2 * ((bh / p.H) * p.ks[0] + (bh % p.H) * p.ks[1]);
   const srd_t ksrd = make_srd(kslice, (int)((int64_t)(p.L - 1) * p.ks[2] * 2 + kRowB));
@@ -454,16 +460,27 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   // issued, past the last tile too (offsets past the table read 0: row 0 into a slot no tile reads
   // any more), so the counts below are constant. Body t needs K(t) and I(t+2); younger than I(t+2)
   // are K(t+1) and S(t-1) (for t = 0: only K1), so K(t+1) stays in flight.
+  // 2-slot ring (36 KiB of LDS: four workgroups per CU): I0 I1 K0, then per body t: I(t+2) K(t+1)
+  // [compute] S(t); K(t+1) can only go after the barrier that frees its slot, so a body waits for
+  // its own K(t) with only S(t-1) younger.
   if (ntiles > 0) {
-    issue_idx(0);
-    issue_idx(1);
-    issue_idx(2);
-    VB_WAIT_VMCNT(2);
-    asm volatile("" ::: "memory");   // the offsets' LDS reads stay behind the wait
-    issue(0);
-    VB_WAIT_VMCNT(1 + kInstPerWave);
-    asm volatile("" ::: "memory");
-    issue(1);
+    if constexpr (kBufs == 2) {
+      issue_idx(0);
+      issue_idx(1);
+      VB_WAIT_VMCNT(1);
+      asm volatile("" ::: "memory");
+      issue(0);
+    } else {
+      issue_idx(0);
+      issue_idx(1);
+      issue_idx(2);
+      VB_WAIT_VMCNT(2);
+      asm volatile("" ::: "memory");   // the offsets' LDS reads stay behind the wait
+      issue(0);
+      VB_WAIT_VMCNT(1 + kInstPerWave);
+      asm volatile("" ::: "memory");
+      issue(1);
+    }
   }
 #else
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
@@ -471,12 +488,21 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
 #if VB_PRED_GATHER
-    if (t == 0) VB_WAIT_VMCNT(kInstPerWave);
-    else VB_WAIT_VMCNT(kInstPerWave + kSt);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue_idx(t + 3);
-    issue(t + 2);
+    if constexpr (kBufs == 2) {
+      if (t == 0) VB_WAIT_VMCNT(0);
+      else VB_WAIT_VMCNT(kSt);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue_idx(t + 2);
+      issue(t + 1);
+    } else {
+      if (t == 0) VB_WAIT_VMCNT(kInstPerWave);
+      else VB_WAIT_VMCNT(kInstPerWave + kSt);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue_idx(t + 3);
+      issue(t + 2);
+    }
 #else
     // retire this wave's DMA of tile t, then the barrier makes every wave's part visible and
     // guarantees tile t-1's buffer is no longer being read. vmcnt counts the R stores too, in issue
@@ -582,18 +608,19 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) mask_predict_kernel
     for (int e = 0; e < 4; ++e) mreg[r + e] = x[e];
   }
   float part = 0.f;
-  // three columns per lane per pass (12 loads in flight; one pass up to nb = 192): the block's 32
-  // row maxima are 64 contiguous bytes
-  for (int j0 = 0; j0 < nb; j0 += 192) {
-    u32x4 w[3][4];
+  // VB_PRED_RCOLS columns per lane per pass (4 loads each in flight): the block's 32 row maxima
+  // are 64 contiguous bytes
+  constexpr int kRC = VB_PRED_RCOLS;
+  for (int j0 = 0; j0 < nb; j0 += 64 * kRC) {
+    u32x4 w[kRC][4];
 #pragma unroll
-    for (int h = 0; h < 3; ++h) {
+    for (int h = 0; h < kRC; ++h) {
       const int jj = min(j0 + 64 * h + lane, nb - 1);
 #pragma unroll
       for (int c = 0; c < 4; ++c) w[h][c] = reinterpret_cast<const u32x4*>(Rq + jj * 32)[c];
     }
 #pragma unroll
-    for (int h = 0; h < 3; ++h) {
+    for (int h = 0; h < kRC; ++h) {
       const int j = j0 + 64 * h + lane;
       float cm = -INFINITY;
 #pragma unroll

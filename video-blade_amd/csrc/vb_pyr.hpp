@@ -48,39 +48,49 @@ __device__ __forceinline__ void kv_pyramid_span(const PyrTask& t, int64_t idx0, 
         if (t.rows) row = t.rows[row];
         x[r] = *reinterpret_cast<const u32x4*>(base + (int64_t)row * s2 * 2);
       }
+      uint8_t* dst1 = dst + (int64_t)(g * 8) * D * 2;
+      uint8_t* dst2 = dst + (int64_t)(off2 + g * 4) * D * 2;
+      uint8_t* dst4 = dst + (int64_t)(off4 + g * 2) * D * 2;
+      uint8_t* dst8 = dst + (int64_t)(off8 + g) * D * 2;
       // level 1 (zero beyond L: the reference kernel's masked loads of the tail block)
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         u32x4 w = x[r];
         if (g * 8 + r >= t.L) w = u32x4{0u, 0u, 0u, 0u};
-        *reinterpret_cast<u32x4*>(dst + (int64_t)(g * 8 + r) * D * 2) = w;
+        *reinterpret_cast<u32x4*>(dst1 + r * D * 2) = w;   // one base, immediate row offsets
       }
-      // levels 2, 4, 8
-      float f[8][8];
+      // levels 2, 4, 8: each level kept as fp32 values of storage-rounded means (x -> f2 -> f4 -> f8)
+      float f2[4][8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r)
+      for (int r = 0; r < 4; ++r) {
+        u32x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const uint32_t u = x[r][e];
-          f[r][2 * e] = T::bits_to_f32((uint16_t)(u & 0xFFFF));
-          f[r][2 * e + 1] = T::bits_to_f32((uint16_t)(u >> 16));
+          const uint32_t a = x[2 * r][e], b = x[2 * r + 1][e];
+          f2[r][2 * e] = round_to<T>((T::bits_to_f32((uint16_t)(a & 0xFFFF)) + T::bits_to_f32((uint16_t)(b & 0xFFFF))) * 0.5f);
+          f2[r][2 * e + 1] = round_to<T>((T::bits_to_f32((uint16_t)(a >> 16)) + T::bits_to_f32((uint16_t)(b >> 16))) * 0.5f);
+          w[e] = pack2<T>(f2[r][2 * e], f2[r][2 * e + 1]);
         }
-      int n = 8;
-      const int lvl_off[3] = {off2, off4, off8};
+        *reinterpret_cast<u32x4*>(dst2 + r * D * 2) = w;
+      }
+      float f4[2][8];
 #pragma unroll
-      for (int lv = 0; lv < 3; ++lv) {
-        n >>= 1;
+      for (int r = 0; r < 2; ++r) {
+        u32x4 w;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (r >= n) break;
-          u32x4 w;
+        for (int e = 0; e < 8; ++e) f4[r][e] = round_to<T>((f2[2 * r][e] + f2[2 * r + 1][e]) * 0.5f);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) f[r][e] = round_to<T>((f[2 * r][e] + f[2 * r + 1][e]) * 0.5f);
+        for (int e = 0; e < 4; ++e) w[e] = pack2<T>(f4[r][2 * e], f4[r][2 * e + 1]);
+        *reinterpret_cast<u32x4*>(dst4 + r * D * 2) = w;
+      }
+      {
+        u32x4 w;
+        float f8[8];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] = pack2<T>(f[r][2 * e], f[r][2 * e + 1]);
-          const int prow = lvl_off[lv] + g * n + r;
-          *reinterpret_cast<u32x4*>(dst + (int64_t)prow * D * 2) = w;
-        }
+        for (int e = 0; e < 8; ++e) f8[e] = round_to<T>((f4[0][e] + f4[1][e]) * 0.5f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = pack2<T>(f8[2 * e], f8[2 * e + 1]);
+        *reinterpret_cast<u32x4*>(dst8) = w;
       }
     }
   }
