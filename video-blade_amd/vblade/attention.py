@@ -142,9 +142,12 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self._kept_slots = None
         self._slot_totals = []
         self.last_mask: Optional[torch.Tensor] = None
-        # optional list: when set, every fused attention launch is bracketed by a pair of HIP
-        # events on the launch stream (bench.py's live kernel timing); None = no events
+        # optional list: when set, every `attn_event_every`-th fused attention launch is bracketed
+        # by a pair of HIP events on the launch stream (bench.py's live kernel timing; each pair is
+        # two marker packets that cost the stream a few us, so the bench samples); None = no events
         self.attn_events: Optional[list] = None
+        self.attn_event_every = 1
+        self._attn_launches = 0
         # run the pooled K/V pass inside the predictor's launch (extra workgroups beside the score
         # workgroups, one stream) instead of as its own launch after it (inference only)
         self.overlap = bool(cfg.get("overlap", True))
@@ -276,6 +279,10 @@ class AdaptiveBlockSparseAttn(nn.Module):
                 kp, vp = pooled
                 k_src, v_src, kv_rows = k, v, rows
             ev = self.attn_events
+            if ev is not None:
+                self._attn_launches += 1
+                if (self._attn_launches - 1) % self.attn_event_every:
+                    ev = None
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
