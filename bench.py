@@ -587,7 +587,10 @@ def measure_backward(variant, dev, reps=6):
             "mask": "energy rule (reference defaults)", "avg_ms": round(ms, 4),
             "flops_per_call": bflops, "achieved": round(tfs, 2), "unit": "TFLOP/s",
             "peak": PEAK_BF16_TFLOPS, "frac": round(tfs / PEAK_BF16_TFLOPS, 4),
-            "launches_timed": reps}
+            "launches_timed": reps,
+            # the deterministic design (no atomics) recomputes S and dP in the dQ kernel: 7 GEMMs
+            # of the forward's size per kept block pair are executed against the 5 counted above
+            "executed_gemm_frac": round(tfs * 7 / 5 / PEAK_BF16_TFLOPS, 4)}
 
 
 def quality_vs_oracle(mod, qkv, variant):
@@ -626,7 +629,7 @@ def quality_vs_oracle(mod, qkv, variant):
                                    "ulp_hist": h_re["ulp_hist"], "max_ulp": h_re["max_ulp"]}}
 
 
-def pmc_traffic(variant, timeout=300, density=None):
+def pmc_traffic(variant, timeout=300, density=None, band=False):
     """HBM-side bytes per attn_fwd_kernel launch from rocprofv3 PMC counters, one counter per
     pass (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
     tallies wide coalesced reads at half their bytes, so traffic = 2*FETCH + WRITE. The target
@@ -640,7 +643,7 @@ def pmc_traffic(variant, timeout=300, density=None):
         d = tempfile.mkdtemp(prefix="vb_pmc_", dir="/tmp")
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.join(ROOT, "tools", "attn_only.py"), variant, "3", "attn",
-               "none" if density is None else str(density)]
+               "none" if density is None else str(density)] + (["band"] if band else [])
         try:
             subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, check=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)

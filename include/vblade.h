@@ -153,6 +153,16 @@ typedef struct vb_predict_args {
    * pool_v, same rows; [B,H,vb_kv_pyramid_rows(L),D] each) run by extra workgroups of the score
    * kernel's launch, like pool_* (which it excludes): no second stream and no events. */
   void* pyr_k; void* pyr_v;
+  /* philox != 0: the two torch.rand(B,H,1,block) draws of random_sample_tokens are generated inside
+   * the sampling launch instead of read from rand_q/rand_k — PyTorch's uniform_ on a device
+   * generator at state (philox_seed, philox_offset): element i of a draw = the x value of the first
+   * hiprand_uniform4 of Philox4x32-10 subsequence i (1.0 mapped to 0.0), the q draw at
+   * philox_offset and the k draw at philox_offset + 4 (each torch.rand call advances the offset by
+   * 4 while B*H*block <= 524288, i.e. one pass of its grid-stride launch). The offsets are WRITTEN
+   * to q_off/k_off; the caller advances its generator by 8. */
+  int philox;
+  uint64_t philox_seed;
+  uint64_t philox_offset;
 } vb_predict_args;
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);

@@ -348,6 +348,46 @@ def test_sample_offsets_match_torch_topk_and_rng_order():
     assert torch.equal(q_off, ref_q) and torch.equal(k_off, ref_k)
 
 
+@pytest.mark.parametrize("B,H,L,D,pre", [(1, 2, 1000, 64, 0), (2, 48, 17776, 64, 3000),
+                                          (1, 12, 32760, 128, 700000), (5, 48, 4096, 64, 17)])
+def test_philox_draws_in_the_sampling_launch_equal_torch_rand(B, H, L, D, pre):
+    """The two draws generated inside the sampling launch (vb_predict_args.philox) are the values
+    torch.rand(B,H,1,128) returns twice on the device's default generator (q first): the scores and
+    mask equal those of the same launch given torch.topk(torch.rand(...)) offsets, and the generator
+    ends at the same state. ``pre`` draws before move the Philox offset off zero (700000 > one
+    grid-stride pass of torch.rand: the offset advances by more than 4)."""
+    from vblade import ops
+    g = torch.Generator().manual_seed(B * 1000 + H)
+    q = torch.randn(B, H, L, D, generator=g).to(torch.bfloat16).to(DEV)
+    k = torch.randn(B, H, L, D, generator=g).to(torch.bfloat16).to(DEV)
+    kw = dict(energy_threshold=0.9, min_keep=2, max_keep=(L + 127) // 128, force_tail=1)
+
+    torch.manual_seed(41)
+    if pre:
+        torch.rand(pre, device=DEV)
+    rq = torch.rand(B, H, 1, 128, device=DEV)
+    rk = torch.rand(B, H, 1, 128, device=DEV)
+    after_ref = torch.rand(7, device=DEV)
+    q_off = torch.topk(rq, 32, dim=3).indices[:, :, 0].to(torch.int32)
+    k_off = torch.topk(rk, 32, dim=3).indices[:, :, 0].to(torch.int32)
+    po_ref, mask_ref = ops.mask_predict(q, k, q_off, k_off, **kw)
+
+    torch.manual_seed(41)
+    if pre:
+        torch.rand(pre, device=DEV)
+    philox = ops.claim_rand_draws(DEV, B * H * 128)
+    assert philox is not None
+    po, mask = ops.mask_predict(q, k, philox=philox, **kw)
+    after = torch.rand(7, device=DEV)
+    assert torch.equal(after, after_ref)
+    assert torch.equal(po, po_ref) and torch.equal(mask, mask_ref)
+
+
+def test_philox_claim_declines_draws_past_one_pass():
+    from vblade import ops
+    assert ops.claim_rand_draws(DEV, ops.RAND_ONE_PASS_NUMEL + 128) is None
+
+
 @pytest.mark.parametrize("n,keep", [(128, 32), (131, 32), (61, 7), (256, 256)])
 def test_sample_offsets_ties_and_ragged_row_lengths(n, keep):
     """The rank loop reads four draws per LDS broadcast with a scalar tail: rows whose length is

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """A/B timing of library variants (video-blade_amd/vblade/variants/lib_<tag>.so) in ONE process on
 ONE GPU: the same inputs, launches interleaved A,B,A,B,... so clock/device drift cancels.
-usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred|call]"""
+usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred|call]
+TAG "cur" is the in-tree libvblade_hip.so; a "@torchrand" suffix runs that tag with the sampling
+draws made by torch.rand instead of inside the sampling launch (ops.PHILOX_DRAWS off)."""
 import argparse
 import ctypes
 import os
@@ -19,7 +21,10 @@ from bench import attn_flops, ml_attn_flops, realistic_qkv  # noqa: E402
 
 
 def load(tag):
+    tag = tag.split("@")[0]
     path = os.path.join(ROOT, "video-blade_amd", "vblade", "variants", f"lib_{tag}.so")
+    if tag == "cur":
+        path = os.path.join(ROOT, "video-blade_amd", "vblade", "libvblade_hip.so")
     lib = ctypes.CDLL(path)
     for name, (res, args) in _lib.SIGNATURES.items():
         try:
@@ -90,6 +95,7 @@ def main():
         with torch.no_grad():
             for t in a.tags:   # warm + cross-check outputs (a repeated tag checks determinism)
                 _lib._lib = libs[t]
+                ops.PHILOX_DRAWS = not t.endswith("@torchrand")
                 out = fn()
                 torch.cuda.synchronize()
                 if a.what == "pred":   # the same scores and energy rule: masks must be identical
@@ -109,6 +115,7 @@ def main():
             for _ in range(a.rounds):
                 for kk, t in zip(keys, a.tags):
                     _lib._lib = libs[t]
+                    ops.PHILOX_DRAWS = not t.endswith("@torchrand")
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(5):

@@ -2,7 +2,10 @@
 """Run only the fused attention kernel (and optionally the predictor) N times on CogVideoX / Wan
 shapes — a target for rocprofv3 counter collection.
 usage: attn_only.py [cog|wan|cog-ml] [N] [attn|pred|all] [density (fixed kept fraction; default:
-the energy rule)]"""
+the energy rule)] [band]
+"band": the predicted mask replaced by a diagonal band with the same kept count per row (plus the
+forced tail rows/columns) — a mask whose neighbouring q-blocks share key blocks, as the synthetic
+random-centre inputs' masks do not (the L2-locality control for the traffic counters)."""
 import os
 import sys
 
@@ -45,6 +48,15 @@ with torch.no_grad():
     qo = vblade.draw_sample_offsets(1, H, dev)
     ko = vblade.draw_sample_offsets(1, H, dev)
     _, mask = m.predict_mask(q, k, qo, ko)
+    if len(sys.argv) > 5 and sys.argv[5] == "band":
+        nb, ft = mask.shape[-1], m.force_tail
+        kk = int(round(mask[..., : nb - ft, :].float().sum(-1).mean().item()))
+        i = torch.arange(nb, device=dev).view(nb, 1)
+        j = torch.arange(nb, device=dev).view(1, nb)
+        lo = (i - kk // 2).clamp(0, nb - kk)
+        band = ((j >= lo) & (j < lo + kk)) | (j >= nb - ft) | (i >= nb - ft)
+        mask = band.to(mask.dtype).expand_as(mask).contiguous()
+        print(f"band mask: {kk} of {nb} blocks per row")
     kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
     # the module's K/V source (gather_kv="auto": gathered rows at D=128, Gilbert copies at D=64), so
     # the counters describe the same kernel variant that bench.py times

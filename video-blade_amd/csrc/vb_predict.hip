@@ -16,6 +16,8 @@
 
 #include <type_traits>
 
+#include <rocrand/rocrand_kernel.h>
+
 #include "vb_tiles.hpp"
 #include "vb_pool.hpp"
 #include "vb_pyr.hpp"
@@ -71,6 +73,7 @@ struct PredParams {
   const int32_t* rows;
   int32_t* q_off; int32_t* k_off;   // inputs, or outputs when rand_q/rand_k are given
   const float* rand_q; const float* rand_k;   // [B,H,block] uniforms (nullable): offsets drawn here
+  int philox; unsigned long long philox_seed, philox_offset;   // or the uniforms generated here
   PoolTask pool;                    // pooled K/V pass run by the first n_pool workgroups (fused launch)
   PyrTask pyr;                      // or the multi-level KV pyramid pass (pool_kind 2)
   int n_pool, pool_kind;
@@ -231,11 +234,35 @@ __device__ __forceinline__ int energy_row(const float* val, uint32_t* keys, uint
 // random_sample_tokens' topk (cogvideo_blocksparseattn.py:45-46) by one wave: the indices of the
 // `keep` largest of n <= 256 uniforms r (global), in descending order of value, ties -> lower index
 // first, written to dst[rank] (LDS or global). `sv` is LDS scratch for n floats.
+__device__ __forceinline__ void topk_wave_lds(int n, int keep, int32_t* dst, const float* sv);
 __device__ __forceinline__ void topk_wave(const float* r, int n, int keep, int32_t* dst, float* sv) {
   const int lane = threadIdx.x & 63;
   for (int i = lane; i < n; i += 64) sv[i] = r[i];
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
+  topk_wave_lds(n, keep, dst, sv);
+}
+
+// torch.rand(B,H,1,block) on a device generator at Philox state (seed, offset), element base + t of
+// the draw for t < n (PyTorch's uniform_: distribution_elementwise_grid_stride_kernel with one
+// grid-stride pass, hiprand_init(seed, element, offset), the x of hiprand_uniform4, 1.0 -> 0.0),
+// written to LDS sv[t] by one wave.
+__device__ __forceinline__ void philox_draw_wave(unsigned long long seed, unsigned long long offset,
+                                                 long long base, int n, float* sv) {
+  const int lane = threadIdx.x & 63;
+  for (int t = lane; t < n; t += 64) {
+    rocrand_state_philox4x32_10 st;
+    rocrand_init(seed, (unsigned long long)(base + t), offset, &st);
+    const float u = rocrand_uniform4(&st).x;
+    sv[t] = u == 1.0f ? 0.0f : u;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// the rank loop of topk_wave on draws already in LDS sv[0..n)
+__device__ __forceinline__ void topk_wave_lds(int n, int keep, int32_t* dst, const float* sv) {
+  const int lane = threadIdx.x & 63;
   // the rank loop reads 4 draws per 16-byte LDS broadcast, 8 reads in flight: a one-float loop was
   // LDS-latency bound (~6 us of sample_rows_kernel's 10 us at the CogVideoX shape)
   const float4* s4 = reinterpret_cast<const float4*>(sv);
@@ -274,7 +301,19 @@ __global__ void __launch_bounds__(256) sample_rows_kernel(const PredParams p) {
   const int bh = blockIdx.y;
   const int wave = threadIdx.x >> 6;
   const int32_t* koff = p.k_off + (int64_t)bh * 32;
-  if (p.rand_k) {
+  if (p.philox) {   // the two torch.rand draws generated here: q at offset, k at offset + 4
+    if (wave == 0) {
+      philox_draw_wave(p.philox_seed, p.philox_offset + 4, (long long)bh * p.block, p.block, sv[0]);
+      topk_wave_lds(p.block, 32, koff_s, sv[0]);
+    }
+    if (blockIdx.x == 0 && wave == 1) {
+      philox_draw_wave(p.philox_seed, p.philox_offset, (long long)bh * p.block, p.block, sv[1]);
+      topk_wave_lds(p.block, 32, p.q_off + (int64_t)bh * 32, sv[1]);
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < 32) p.k_off[(int64_t)bh * 32 + threadIdx.x] = koff_s[threadIdx.x];
+    koff = koff_s;
+  } else if (p.rand_k) {
     if (wave == 0) topk_wave(p.rand_k + (int64_t)bh * p.block, p.block, 32, koff_s, sv[0]);
     if (blockIdx.x == 0 && wave == 1)
       topk_wave(p.rand_q + (int64_t)bh * p.block, p.block, 32, p.q_off + (int64_t)bh * 32, sv[1]);
@@ -773,6 +812,12 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   if ((a->rand_q == nullptr) != (a->rand_k == nullptr))
     return fail(VB_ERR_INVALID, "vb_mask_predict: give both rand_q and rand_k or neither");
   p.rand_q = a->rand_q; p.rand_k = a->rand_k;
+  if (a->philox) {
+    if (a->rand_q || a->rand_k) return fail(VB_ERR_INVALID, "vb_mask_predict: philox and rand_q/rand_k are exclusive");
+    if ((int64_t)a->B * a->H * a->block > 524288)
+      return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: philox draws need B*H*block <= 524288");
+    p.philox = 1; p.philox_seed = a->philox_seed; p.philox_offset = a->philox_offset;
+  }
   if (a->pool_kp) {   // the pooled K/V pass rides in the score kernel's launch
     if (!a->pool_v || !a->pool_vp || a->pool_gap <= 0 || ((a->pool_k_r == nullptr) != (a->pool_v_r == nullptr)))
       return fail(VB_ERR_INVALID, "vb_mask_predict: pool_v, pool_vp, pool_gap > 0 and both or neither of pool_k_r/pool_v_r");

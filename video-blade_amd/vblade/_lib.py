@@ -58,6 +58,7 @@ class PredictArgs(ctypes.Structure):
         ("pool_v", _vp), ("pool_v_stride", _i64x3), ("pool_gap", ctypes.c_int),
         ("pool_kp", _vp), ("pool_vp", _vp), ("pool_k_r", _vp), ("pool_v_r", _vp),
         ("pyr_k", _vp), ("pyr_v", _vp),
+        ("philox", ctypes.c_int), ("philox_seed", ctypes.c_uint64), ("philox_offset", ctypes.c_uint64),
     ]
 
 

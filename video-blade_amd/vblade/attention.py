@@ -206,11 +206,14 @@ class AdaptiveBlockSparseAttn(nn.Module):
         """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores. ``pool``
         (v, gap, outs) runs the pooled K/V pass inside the score kernel's launch."""
         B, H, L, D = q.shape
-        rand = None
+        rand = philox = None
         if q_off is None and k_off is None:
-            # the reference's two draws (:77-78, q first); topk runs inside the sampling launch
-            rand = (torch.rand(B, H, 1, self.block, device=q.device),
-                    torch.rand(B, H, 1, self.block, device=q.device))
+            # the reference's two draws (:77-78, q first), generated and ranked inside the sampling
+            # launch at the device generator's Philox state (the values torch.rand would return)
+            philox = ops.claim_rand_draws(q.device, B * H * self.block)
+            if philox is None:
+                rand = (torch.rand(B, H, 1, self.block, device=q.device),
+                        torch.rand(B, H, 1, self.block, device=q.device))
         elif q_off is None:
             q_off = draw_sample_offsets(B, H, q.device)
         elif k_off is None:
@@ -220,7 +223,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
         po, mask = ops.mask_predict(q, k, q_off, k_off, rows=self._rows(q.device),
                                     energy_threshold=self.energy_threshold, min_keep=lo,
                                     max_keep=hi, force_tail=self.force_tail, mask_count=count,
-                                    staged_event=staged_event, rand=rand, pool=pool)
+                                    staged_event=staged_event, rand=rand, philox=philox,
+                                    pool=pool)
         return po, mask
 
     def forward(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *,

@@ -49,14 +49,17 @@ def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=N
     q, k: returns (po [B,H,nb,nb] q.dtype, level mask uint8 [B,H,nb,nb]). ``pyr=(v, outs)``: the
     KV pyramid pass in the score kernel's launch (ops.mask_predict)."""
     B, H, L, D = q.shape
-    rand = None
+    rand = philox = None
     if q_off is None and k_off is None:
-        # the reference's two draws (:77-78, q first); topk runs inside the sampling launch, as in
-        # AdaptiveBlockSparseAttn.predict_mask (one launch less than vb_sample_offsets + predict)
-        rand = (torch.rand(B, H, 1, BLOCK, device=q.device), torch.rand(B, H, 1, BLOCK, device=q.device))
+        # the reference's two draws (:77-78, q first), generated and ranked inside the sampling
+        # launch, as in AdaptiveBlockSparseAttn.predict_mask
+        philox = ops.claim_rand_draws(q.device, B * H * BLOCK)
+        if philox is None:
+            rand = (torch.rand(B, H, 1, BLOCK, device=q.device), torch.rand(B, H, 1, BLOCK, device=q.device))
     elif q_off is None or k_off is None:
         q_off, k_off = draw_sample_offsets_qk(B, H, q.device, BLOCK, 32)
-    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, rand=rand, pyr=pyr)
+    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, rand=rand, philox=philox,
+                             pyr=pyr)
     return po, ops.level_mask(po, mask_ratios)
 
 

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Optional
 
 import numpy as np
@@ -283,7 +284,7 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
 # ----------------------------------------------------------------------------------------------
 def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.95, min_keep=1,
                  max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True,
-                 staged_event=None, rand=None, pool=None, pyr=None):
+                 staged_event=None, rand=None, philox=None, pool=None, pyr=None):
     """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
     po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb] (None with want_mask=False: the scores
     only, no energy rule). ``staged_event`` (a torch.cuda.Event) is recorded once the sampled
@@ -291,6 +292,8 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
 
     ``rand=(rand_q, rand_k)``: the fp32 uniforms [B,H,1,block] of random_sample_tokens instead of
     q_off/k_off; the topk offsets are drawn inside the sampling launch.
+    ``philox=(seed, offset)`` (from claim_rand_draws): those two draws generated inside the
+    sampling launch too, equal to the values torch.rand would return at that generator state.
     ``pool=(v, gap, outs)``: the pooled K/V pass (vb_pool_kv of k, v through ``rows``) run by extra
     workgroups of the score kernel's launch on the current stream; ``outs`` = pool_kv_outputs(k,
     gap, reordered) receives kp, vp[, k_r, v_r].
@@ -305,8 +308,11 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     nb = (L + BLOCK - 1) // BLOCK
     po = torch.empty(B, H, nb, nb, device=dev, dtype=q.dtype)
     mask = torch.empty(B, H, nb, nb, device=dev, dtype=torch.uint8) if want_mask else None
-    if rand is not None:
-        rand_q, rand_k = (r.float().contiguous() for r in rand)
+    if rand is not None and philox is not None:
+        raise ValueError("mask_predict: rand and philox are exclusive")
+    if rand is not None or philox is not None:
+        if rand is not None:
+            rand_q, rand_k = (r.float().contiguous() for r in rand)
         q_off = torch.empty(B, H, 32, device=dev, dtype=torch.int32)
         k_off = torch.empty(B, H, 32, device=dev, dtype=torch.int32)
     q_off = q_off.to(torch.int32).contiguous()
@@ -330,6 +336,8 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
         if rand_q.shape[-1] != BLOCK or rand_q.numel() != B * H * BLOCK or rand_k.numel() != B * H * BLOCK:
             raise ValueError("mask_predict: rand draws must be [B,H,1,block]")
         a.rand_q, a.rand_k = rand_q.data_ptr(), rand_k.data_ptr()
+    if philox is not None:
+        a.philox, a.philox_seed, a.philox_offset = 1, int(philox[0]), int(philox[1])
     if pool is not None:
         v, gap, outs = pool
         v = _aligned_bhld(v)
@@ -356,6 +364,26 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
         a.pyr_k, a.pyr_v = outs[0].data_ptr(), outs[1].data_ptr()
     check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
+
+
+# torch.rand's launch on ROCm (ATen/native/hip/DistributionTemplates.h): one grid-stride pass of
+# 256-thread blocks, 4 uniforms per thread, while numel <= 256 * (CUs * 2048 / 256) * 4; each call
+# then advances the generator's Philox offset by 4. 524288 = that bound at 256 CUs.
+RAND_ONE_PASS_NUMEL = 524288
+PHILOX_DRAWS = os.environ.get("VB_PHILOX_DRAWS", "1") != "0"   # off: the callers use torch.rand
+
+
+def claim_rand_draws(device, numel: int, draws: int = 2):
+    """Reserve ``draws`` consecutive torch.rand(numel) calls on ``device``'s default generator for
+    a kernel that generates them itself: returns (seed, offset) and advances the generator's offset
+    as those calls would, or None when the draw is too large for one pass (then call torch.rand)."""
+    if numel > RAND_ONE_PASS_NUMEL or not PHILOX_DRAWS:
+        return None
+    dev = torch.device(device)
+    gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+    seed, off = gen.initial_seed(), gen.get_offset()
+    gen.set_offset(off + 4 * draws)
+    return seed, off
 
 
 def sample_offsets(rand_q, rand_k, keep: int = 32):
