@@ -163,6 +163,17 @@ typedef struct vb_predict_args {
   int philox;
   uint64_t philox_seed;
   uint64_t philox_offset;
+  /* mask_level != 0: `mask` receives the multi-level rank-band mask instead of the energy mask —
+   * vb_level_mask's rule (bands level_band_value / [level_band_start, level_band_end) as fractions
+   * of nb, 0..8 of them; the last two rows and columns forced to level 1) applied by the score
+   * kernel's epilogue to the normalised scores it has just written to po: no second launch and no
+   * re-read of po. Replaces the vb_level_mask launch of the multi-level path
+   * (Triton/cogvideo_newattn.py:154-207). */
+  int mask_level;
+  int level_bands;
+  const int32_t* level_band_value;
+  const double* level_band_start;
+  const double* level_band_end;
 } vb_predict_args;
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);

@@ -135,6 +135,29 @@ def test_level_mask_kernel_matches_oracle(nr, nc):
     assert torch.equal(mask, ML.level_mask(po, ratios))
 
 
+@pytest.mark.parametrize("L,D,B,H,ratios", [(17776, 64, 1, 2, None), (32760, 128, 1, 1, None),
+                                             (1000, 64, 2, 3, None), (300, 128, 1, 2, "overlap"),
+                                             (17776, 64, 1, 1, "empty")])
+def test_level_mask_in_the_score_kernel_equals_vb_level_mask(L, D, B, H, ratios):
+    """The level mask written by the score kernel's epilogue (ops.mask_predict level=..., the
+    multi-level module's path) equals vb_level_mask on the scores the same launch returns, bit for
+    bit: the reference bands, overlapping bands (later wins) and no bands (forced tail only).
+    Low-entropy inputs make many exactly tied bf16 scores (ties -> lower column)."""
+    ops = _ops()
+    r = {None: None, "overlap": {8: (0.0, 0.3), 2: (0.2, 0.6), 0: (0.6, 1.0)}, "empty": {}}[ratios]
+    g = torch.Generator(device=DEV).manual_seed(L + H)
+    q = (torch.randn(B, H, L, D, generator=g, device=DEV) * 0.05).bfloat16()
+    k = (torch.randn(B, H, L, D, generator=g, device=DEV) * 0.05).bfloat16()
+    rows = torch.randperm(L, generator=torch.Generator().manual_seed(9)).int().to(DEV)
+    rq = torch.rand(B, H, 1, 128, device=DEV, generator=g)
+    rk = torch.rand(B, H, 1, 128, device=DEV, generator=g)
+    po, mask = ops.mask_predict(q, k, rows=rows, rand=(rq, rk), level=ops.ML_MASK_RATIOS if r is None else r)
+    po2, _ = ops.mask_predict(q, k, rows=rows, want_mask=False, rand=(rq, rk))
+    assert torch.equal(po, po2)
+    assert torch.equal(mask, ops.level_mask(po, r))
+    assert torch.equal(mask.cpu().to(torch.int32), ML.level_mask(po.cpu(), r))
+
+
 # ------------------------------------------------------------------------------------- forward
 @pytest.mark.parametrize("case", ["f16_d64", "f16_d128_b2"])
 def test_ml_forward_matches_reference_kernel_fixture(case):

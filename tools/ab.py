@@ -3,7 +3,8 @@
 ONE GPU: the same inputs, launches interleaved A,B,A,B,... so clock/device drift cancels.
 usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred|call]
 TAG "cur" is the in-tree libvblade_hip.so; a "@torchrand" suffix runs that tag with the sampling
-draws made by torch.rand instead of inside the sampling launch (ops.PHILOX_DRAWS off)."""
+draws made by torch.rand instead of inside the sampling launch (ops.PHILOX_DRAWS off), "@lvsep"
+with the multi-level mask as its own vb_level_mask launch (--what mlcall: the multi-level module)."""
 import argparse
 import ctypes
 import os
@@ -16,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)
 import vblade  # noqa: E402
-from vblade import _lib, ops  # noqa: E402
+from vblade import _lib, multilevel, ops  # noqa: E402
 from bench import attn_flops, ml_attn_flops, realistic_qkv  # noqa: E402
 
 
@@ -81,13 +82,15 @@ def main():
                                            alpha=alpha, gap=gap, heavy_rows=m.force_tail)
             fl = 2.5 * fl
         elif a.what == "mlbwd":   # the multi-level path's backward (vb_ml_attn_bwd), dk compared
-            from vblade import multilevel
             do = torch.randn_like(q)
             _, lmask = multilevel.predict_level_mask(q, k, rows=rows)
             kpy, vpy = ops.kv_pyramid(k, v, rows)
             mo, mlse = ops.ml_attention_fwd(q, kpy, vpy, lmask, q_rows=rows, want_lse=True, heavy_rows=2)
             fn = lambda: ops.ml_attention_bwd(do, q, kpy, vpy, lmask, mo, mlse, rows=rows)[1]  # noqa
             fl = 2.5 * ml_attn_flops(lmask, L, D)
+        elif a.what == "mlcall":   # the multi-level (VBench) module, whole call
+            mlm = multilevel.AdaptiveBlockSparseAttnTrain(log_every=0)
+            fn = lambda: mlm(q, k, v)  # noqa
         else:
             fn = lambda: m(q, k, v)  # noqa
         ref = None
@@ -96,6 +99,7 @@ def main():
             for t in a.tags:   # warm + cross-check outputs (a repeated tag checks determinism)
                 _lib._lib = libs[t]
                 ops.PHILOX_DRAWS = not t.endswith("@torchrand")
+                multilevel.FUSED_LEVEL_MASK = not t.endswith("@lvsep")
                 out = fn()
                 torch.cuda.synchronize()
                 if a.what == "pred":   # the same scores and energy rule: masks must be identical
@@ -116,6 +120,7 @@ def main():
                 for kk, t in zip(keys, a.tags):
                     _lib._lib = libs[t]
                     ops.PHILOX_DRAWS = not t.endswith("@torchrand")
+                    multilevel.FUSED_LEVEL_MASK = not t.endswith("@lvsep")
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(5):

@@ -65,6 +65,12 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int kFusedPoolWgs = VB_FUSED_POOL_WGS;
 
+// multi-level rank bands (value, [start, end) in ranks) for the fused level-mask epilogue
+struct PredBands {
+  int n;
+  int value[8], start[8], end[8];
+};
+
 struct PredParams {
   const void* q; const void* k;
   int64_t qs[3], ks[3];
@@ -77,6 +83,8 @@ struct PredParams {
   PoolTask pool;                    // pooled K/V pass run by the first n_pool workgroups (fused launch)
   PyrTask pyr;                      // or the multi-level KV pyramid pass (pool_kind 2)
   int n_pool, pool_kind;
+  int level;        // 1: the epilogue writes the multi-level rank-band mask (bands lv), not the energy mask
+  PredBands lv;
   int B, H, L, D, block, nb;
   float c;             // fp32(scale) * fp32(1.44269504), as the Triton kernel forms qk_scale
   float thr;
@@ -113,12 +121,11 @@ __device__ __forceinline__ uint32_t storage_bits(float v) {
 // first (a stable descending sort), one unsigned compare per pair. The fp32-accumulated
 // cumulative sum over the sorted values runs sequentially (bit-identical to torch's CPU cumsum)
 // as one uniform chain; lane t keeps the prefix at its own position where the clamp can see it.
+// The stable descending rank of each of the lane's U values (columns lane + 64u), by one wave.
 template <class T, int U>
-__device__ __forceinline__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
-                            int min_keep, int max_keep, int force_cols, bool force_all) {
+__device__ __forceinline__ void row_ranks(const float* val, uint32_t* keys, int nc, int (&rank)[U]) {
   const int lane = threadIdx.x & 63;
   uint32_t mykey[U];
-  int rank[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int j = lane + 64 * u;
@@ -143,6 +150,15 @@ __device__ __forceinline__ int energy_row_u(const float* val, uint32_t* keys, ui
 #pragma unroll
         for (int u = 0; u < U; ++u) rank[u] += (kk[c][e] > mykey[u]) ? 1 : 0;
   }
+}
+
+template <class T, int U>
+__device__ __forceinline__ int energy_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int nc, float thr,
+                            int min_keep, int max_keep, int force_cols, bool force_all) {
+  const int lane = threadIdx.x & 63;
+  int rank[U];
+  row_ranks<T, U>(val, keys, nc, rank);
+  const int nc16 = (nc + 15) & ~15;
   // scatter values into sorted order (reuse `keys` as float storage after a wave barrier)
   __builtin_amdgcn_wave_barrier();
   float* sorted = reinterpret_cast<float*>(keys);
@@ -228,6 +244,38 @@ __device__ __forceinline__ int energy_row(const float* val, uint32_t* keys, uint
     case 4: return energy_row_u<T, 4>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols, force_all);
     default: return energy_row_u<T, (kMaxNb + 63) / 64>(val, keys, mrow, nc, thr, min_keep, max_keep, force_cols,
                                                            force_all);
+  }
+}
+
+// Multi-level rank bands (transfer_attn_to_mask, Triton/cogvideo_newattn.py:154-207; vb_level_mask's
+// rule, vb_ml.hip) on one row of normalised scores in LDS `val`: the column of stable descending rank
+// r gets the value of the last band whose [start, end) holds r (0 if none); the last two rows and
+// columns are forced to level 1. Ranks as the energy rule's (same keys), so ties go to the lower column.
+template <class T, int U>
+__device__ __forceinline__ void level_row_u(const float* val, uint32_t* keys, uint8_t* mrow, int nc, int row,
+                                            const PredBands& lv) {
+  const int lane = threadIdx.x & 63;
+  int rank[U];
+  row_ranks<T, U>(val, keys, nc, rank);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = lane + 64 * u;
+    int l = 0;
+    for (int b = 0; b < lv.n; ++b)
+      if (rank[u] >= lv.start[b] && rank[u] < lv.end[b]) l = lv.value[b];
+    if (j >= nc - 2 || row >= nc - 2) l = 1;
+    if (j < nc) mrow[j] = (uint8_t)l;
+  }
+}
+template <class T>
+__device__ __forceinline__ void level_row(const float* val, uint32_t* keys, uint8_t* mrow, int nc, int row,
+                                          const PredBands& lv) {
+  switch ((nc + 63) >> 6) {
+    case 1: return level_row_u<T, 1>(val, keys, mrow, nc, row, lv);
+    case 2: return level_row_u<T, 2>(val, keys, mrow, nc, row, lv);
+    case 3: return level_row_u<T, 3>(val, keys, mrow, nc, row, lv);
+    case 4: return level_row_u<T, 4>(val, keys, mrow, nc, row, lv);
+    default: return level_row_u<T, (kMaxNb + 63) / 64>(val, keys, mrow, nc, row, lv);
   }
 }
 
@@ -689,6 +737,10 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
   uint8_t* mrow = p.mask + ((int64_t)bh * nb + qb) * nb;
+  if (p.level) {   // the multi-level path's rank bands instead of the energy rule
+    level_row<T>(val, keys, mrow, nb, qb, p.lv);
+    return;
+  }
   const bool force_all = p.force_tail > 0 && qb >= nb - p.force_tail;
   const int kept = energy_row<T>(val, keys, mrow, nb, p.thr, p.min_keep, p.max_keep, p.force_tail, force_all);
   if (p.count && lane == 0) atomicAdd(p.count, (unsigned long long)kept);
@@ -812,6 +864,24 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   if ((a->rand_q == nullptr) != (a->rand_k == nullptr))
     return fail(VB_ERR_INVALID, "vb_mask_predict: give both rand_q and rand_k or neither");
   p.rand_q = a->rand_q; p.rand_k = a->rand_k;
+  if (a->level_bands < 0 || a->level_bands > 8 ||
+      (a->level_bands > 0 && (!a->level_band_value || !a->level_band_start || !a->level_band_end)))
+    return fail(VB_ERR_INVALID, "vb_mask_predict: 0..8 level bands with value/start/end arrays");
+  if (a->mask_level) {
+    if (!a->mask) return fail(VB_ERR_INVALID, "vb_mask_predict: mask_level needs a mask output");
+    p.level = 1;
+    p.lv.n = a->level_bands;
+    for (int i = 0; i < a->level_bands; ++i) {
+      const int val = a->level_band_value[i];
+      if (val != 0 && val != 1 && val != 2 && val != 4 && val != 8)
+        return fail(VB_ERR_INVALID, "vb_mask_predict: band values must be 0, 1, 2, 4 or 8");
+      // max(0, int(nb * start)), min(nb, int(nb * end)) in double, as vb_level_mask
+      const int ia = (int)((double)nb * a->level_band_start[i]), ib = (int)((double)nb * a->level_band_end[i]);
+      p.lv.value[i] = val;
+      p.lv.start[i] = ia < 0 ? 0 : ia;
+      p.lv.end[i] = ib > nb ? nb : ib;
+    }
+  }
   if (a->philox) {
     if (a->rand_q || a->rand_k) return fail(VB_ERR_INVALID, "vb_mask_predict: philox and rand_q/rand_k are exclusive");
     if ((int64_t)a->B * a->H * a->block > 524288)

@@ -59,6 +59,8 @@ class PredictArgs(ctypes.Structure):
         ("pool_kp", _vp), ("pool_vp", _vp), ("pool_k_r", _vp), ("pool_v_r", _vp),
         ("pyr_k", _vp), ("pyr_v", _vp),
         ("philox", ctypes.c_int), ("philox_seed", ctypes.c_uint64), ("philox_offset", ctypes.c_uint64),
+        ("mask_level", ctypes.c_int), ("level_bands", ctypes.c_int),
+        ("level_band_value", _vp), ("level_band_start", _vp), ("level_band_end", _vp),
     ]
 
 

@@ -14,11 +14,12 @@ cogvideox/sample_evaluate/modify_cogvideo.py:9):
     [B,H,nb,nb] int level mask (0 skip, 1/2/4/8 = K/V mean-pooled by that factor, +ln p logit bias).
 
 Every tensor op runs in libvblade_hip.so:
-  1. vb_mask_predict (the rand draws ranked inside its sampling launch) — sampled pooled scores
-     (Gilbert order through ``rows``); the KV pyramid pass (one pass over K/V: reordered level-1
-     rows + 2x/4x/8x pooled rows, HBM-bound) runs as extra workgroups of the score kernel's launch
-  2. vb_level_mask  — rank bands -> uint8 level mask
-  3. vb_ml_attn_fwd — one softmax over every kept block's keys at its level; q rows gathered and
+  1. vb_mask_predict (the rand draws generated and ranked inside its sampling launch) — sampled
+     pooled scores (Gilbert order through ``rows``) and, in the score kernel's epilogue, the rank
+     bands -> uint8 level mask (vb_level_mask's rule, ``mask_level``); the KV pyramid pass (one
+     pass over K/V: reordered level-1 rows + 2x/4x/8x pooled rows, HBM-bound) runs as extra
+     workgroups of the same launch
+  2. vb_ml_attn_fwd — one softmax over every kept block's keys at its level; q rows gathered and
                       out rows scattered through the Gilbert index inside the kernel
 """
 from __future__ import annotations
@@ -35,6 +36,7 @@ from .attention import GilbertRearranger, draw_sample_offsets_qk
 MASK_RATIOS = dict(ops.ML_MASK_RATIOS)
 DEFAULTS = dict(use_rearrange=True, width=45, height=30, depth=13, text_length=226)
 BLOCK = 128
+FUSED_LEVEL_MASK = True   # False: the level mask as its own vb_level_mask launch (A/B timing only)
 
 
 def density(mask_ratios=None) -> float:
@@ -58,9 +60,14 @@ def predict_level_mask(q, k, *, rows=None, mask_ratios=None, q_off=None, k_off=N
             rand = (torch.rand(B, H, 1, BLOCK, device=q.device), torch.rand(B, H, 1, BLOCK, device=q.device))
     elif q_off is None or k_off is None:
         q_off, k_off = draw_sample_offsets_qk(B, H, q.device, BLOCK, 32)
-    po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, rand=rand, philox=philox,
-                             pyr=pyr)
-    return po, ops.level_mask(po, mask_ratios)
+    # the rank-band level mask comes out of the score kernel's epilogue (vb_predict_args.mask_level;
+    # ops.level_mask is the stand-alone form of the same rule)
+    if not FUSED_LEVEL_MASK:
+        po, _ = ops.mask_predict(q, k, q_off, k_off, rows=rows, want_mask=False, rand=rand, philox=philox,
+                                 pyr=pyr)
+        return po, ops.level_mask(po, mask_ratios)
+    return ops.mask_predict(q, k, q_off, k_off, rows=rows, rand=rand, philox=philox, pyr=pyr,
+                            level=MASK_RATIOS if mask_ratios is None else mask_ratios)
 
 
 def adaptive_block_sparse_attn(q, k, v, *, rows=None, mask_ratios=None, ref_tail=True,

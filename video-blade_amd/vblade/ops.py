@@ -284,7 +284,7 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
 # ----------------------------------------------------------------------------------------------
 def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.95, min_keep=1,
                  max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True,
-                 staged_event=None, rand=None, philox=None, pool=None, pyr=None):
+                 staged_event=None, rand=None, philox=None, pool=None, pyr=None, level=None):
     """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
     po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb] (None with want_mask=False: the scores
     only, no energy rule). ``staged_event`` (a torch.cuda.Event) is recorded once the sampled
@@ -298,7 +298,9 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     workgroups of the score kernel's launch on the current stream; ``outs`` = pool_kv_outputs(k,
     gap, reordered) receives kp, vp[, k_r, v_r].
     ``pyr=(v, outs)``: the multi-level KV pyramid pass (vb_kv_pyramid of k, v through ``rows``)
-    run the same way; ``outs`` = kv_pyramid_outputs(k). Excludes ``pool``."""
+    run the same way; ``outs`` = kv_pyramid_outputs(k). Excludes ``pool``.
+    ``level=mask_ratios``: the returned mask is the multi-level rank-band mask (level_mask's rule
+    on the scores, computed by the score kernel's epilogue) instead of the energy mask."""
     if k.shape != q.shape:
         raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
                          f"got k {tuple(k.shape)}")
@@ -362,6 +364,13 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
             raise ValueError("mask_predict: pyramid outputs must come from kv_pyramid_outputs(k)")
         a.pool_v, a.pool_v_stride = v.data_ptr(), _s3(v)
         a.pyr_k, a.pyr_v = outs[0].data_ptr(), outs[1].data_ptr()
+    if level is not None:
+        if mask is None:
+            raise ValueError("mask_predict: level needs want_mask=True")
+        vals, st, en = _level_bands(level)
+        a.mask_level, a.level_bands = 1, len(vals)
+        a.level_band_value, a.level_band_start, a.level_band_end = (
+            vals.ctypes.data, st.ctypes.data, en.ctypes.data)
     check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
 
@@ -526,16 +535,24 @@ def pyramid_levels(pyr: torch.Tensor, L: int):
     return [pyr[:, :, offs[i]:offs[i + 1]] for i in range(4)]
 
 
+def _level_bands(ratios):
+    """mask_ratios {level: (start, end)} -> (int32 values, float64 starts, float64 ends), dict order."""
+    ratios = ML_MASK_RATIOS if ratios is None else ratios
+    vals = np.array([int(v) for v in ratios], dtype=np.int32)
+    st = np.array([float(r[0]) for r in ratios.values()], dtype=np.float64)
+    en = np.array([float(r[1]) for r in ratios.values()], dtype=np.float64)
+    if len(vals) > 8:
+        raise ValueError("level mask: at most 8 bands")
+    return vals, st, en
+
+
 def level_mask(po, ratios=None):
     """vb_level_mask: transfer_attn_to_mask (Triton/cogvideo_newattn.py:154-207) on scores po
     [B,H,nr,nc] -> uint8 levels (ties: lower column first)."""
     dev = _require_gpu(po)
     po = po.contiguous()
     B, H, nr, nc = po.shape
-    ratios = ML_MASK_RATIOS if ratios is None else ratios
-    vals = np.array([int(v) for v in ratios], dtype=np.int32)
-    st = np.array([float(r[0]) for r in ratios.values()], dtype=np.float64)
-    en = np.array([float(r[1]) for r in ratios.values()], dtype=np.float64)
+    vals, st, en = _level_bands(ratios)
     mask = torch.empty(B, H, nr, nc, device=dev, dtype=torch.uint8)
     check(_lib.load().vb_level_mask(po.data_ptr(), B, H, nr, nc, len(vals), vals.ctypes.data,
                                     st.ctypes.data, en.ctypes.data, _dtype_code(po), mask.data_ptr(),
