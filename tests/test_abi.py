@@ -131,6 +131,53 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     assert rc == _lib.VB_ERR_INVALID and b"band values" in lib.vb_last_error()
 
 
+def test_mask_predict_option_checks_without_gpu(lib):
+    """vb_mask_predict's host-side checks of the round-3 options run before any launch: Philox
+    draws exclusive with rand_q/rand_k and limited to one torch.rand grid-stride pass, level bands
+    validated and needing a mask output."""
+    from vblade import _lib
+    def args(B=1, H=2, L=1000):
+        p = _lib.PredictArgs()
+        p.q = p.k = p.q_off = p.k_off = p.po = p.mask = 1 << 20
+        p.B, p.H, p.L, p.D, p.block, p.num_keep = B, H, L, 64, 128, 32
+        p.q_stride = p.k_stride = (H * L * 64, L * 64, 64)
+        p.min_keep = p.max_keep = 1
+        p.workspace = 1 << 24
+        p.workspace_bytes = lib.vb_mask_predict_workspace_size(ctypes.byref(p))
+        return p
+    p = args()
+    p.philox, p.rand_q, p.rand_k = 1, 1 << 20, 1 << 20
+    assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
+    assert b"exclusive" in lib.vb_last_error()
+    p = args(B=2, H=2049)                         # 2*2049*128 > 524288
+    p.philox = 1
+    assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_UNSUPPORTED
+    assert b"524288" in lib.vb_last_error()
+    vals = np.array([3], dtype=np.int32)
+    se = np.array([0.0, 1.0], dtype=np.float64)
+    p = args()
+    p.mask_level, p.level_bands = 1, 1
+    p.level_band_value, p.level_band_start, p.level_band_end = vals.ctypes.data, se[:1].ctypes.data, se[1:].ctypes.data
+    assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
+    assert b"band values" in lib.vb_last_error()
+    p = args()
+    p.mask_level, p.level_bands, p.level_band_value = 1, 9, vals.ctypes.data
+    assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
+    p = args()
+    p.mask, p.mask_level = None, 1
+    assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
+    assert b"mask output" in lib.vb_last_error()
+
+
+def test_level_bands_follow_mask_ratio_dict_order():
+    from vblade import ops
+    vals, st, en = ops._level_bands({8: (0.25, 0.5), 1: (0.0, 0.05)})
+    assert vals.tolist() == [8, 1] and st.tolist() == [0.25, 0.0] and en.tolist() == [0.5, 0.05]
+    vals, _, _ = ops._level_bands(None)
+    assert vals.tolist() == [int(v) for v in ops.ML_MASK_RATIOS]
+    assert ops.claim_rand_draws("cuda", ops.RAND_ONE_PASS_NUMEL + 1) is None   # past one pass: torch.rand
+
+
 def test_ops_refuse_cpu_tensors():
     """The product path has no CPU fallback: CPU tensors raise."""
     import torch
