@@ -186,6 +186,9 @@ __global__ void __launch_bounds__(256) bwd_prep_kernel(const PrepParams p) {
 #ifndef VB_DKDV_WAVES_D64
 #define VB_DKDV_WAVES_D64 2   // waves per SIMD the D=64 dK/dV kernel is register-budgeted for
 #endif
+#ifndef VB_ML_LONG_FIRST
+#define VB_ML_LONG_FIRST 1   // multi-level pooled dK/dV items in level 8, 4, 2 order (longest first; 0: 2, 4, 8)
+#endif
 template <int D, class T, bool kPooled, bool kML = false>
 __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D64) bwd_dkdv_kernel(const BwdParams p) {
   using namespace bwd;
@@ -222,7 +225,19 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   // XCD's range left a long tail (measured: 1.26 waves per SIMD on average at 2 possible).
   const int split = kPooled ? (int)blockIdx.x % p.psplit : 0;
   int bh, kblk;
-  if (kPooled) {
+  int ml_e = 0, ml_m = 0;   // multi-level pooled items: level exponent and pyramid block
+  if (kML && kPooled && VB_ML_LONG_FIRST) {
+    // longest items first: a level-8 block's q-list is the union over 8 key blocks (≈4x a level-2
+    // item's tiles), so level 8, then 4, then 2, each spread over the heads (consecutive
+    // workgroups = different heads, so different XCDs); placement only, the results are the same
+    const MlGeom gm(p.Lpad);
+    int lin = (int)blockIdx.x;
+    ml_e = 3;
+    while (ml_e > 1 && lin >= gm.nblk[ml_e] * BH) { lin -= gm.nblk[ml_e] * BH; --ml_e; }
+    bh = lin % BH;
+    ml_m = lin / BH;
+    kblk = 0;
+  } else if (kPooled) {
     const int lin = (int)blockIdx.x / p.psplit;
     bh = lin / nkb;
     kblk = lin % nkb;
@@ -251,10 +266,11 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   int k0 = kblk * kBlk;
   // multi-level: level e (p = 2^e) of this work item, its pyramid region start and row count;
   // pooled items number the level-2, then level-4, then level-8 pyramid blocks
-  int ml_e = 0, ml_m = kblk, ml_row0 = 0;
+  int ml_row0 = 0;
+  if (!(kML && kPooled && VB_ML_LONG_FIRST)) ml_m = kblk;
   if (kML) {
     const MlGeom gm(p.Lpad);
-    if (kPooled) {
+    if (kPooled && !VB_ML_LONG_FIRST) {
       ml_e = 1;
       while (ml_e < 3 && ml_m >= gm.nblk[ml_e]) { ml_m -= gm.nblk[ml_e]; ++ml_e; }
     }
