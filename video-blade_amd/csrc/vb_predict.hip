@@ -98,6 +98,22 @@ struct PredParams {
 #ifndef VB_DIAG
 #define VB_DIAG 0
 #endif
+#ifndef VB_PRED_STAMPS
+#define VB_PRED_STAMPS 0   // diagnostic builds only (tools/pred_stamps.py): per-phase s_memtime sums
+#endif
+#if VB_PRED_STAMPS
+__device__ unsigned long long g_pred_stamp[8];
+__device__ __forceinline__ unsigned long long pred_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define VB_PST(var) const unsigned long long var = pred_stamp()
+#else
+#define VB_PST(var)
+#endif
 
 // caller row holding reordered-padded position `pos` of a (b,h) stream
 __device__ __forceinline__ int sampled_row(int blk, int off, int block, int L, const int32_t* rows) {
@@ -572,8 +588,12 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
 #else
   for (int t = 0; t < kBufs - 1 && t < ntiles; ++t) issue(t);
 #endif
+#if VB_PRED_STAMPS
+  unsigned long long pst[4] = {0, 0, 0, 0};
+#endif
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
+    VB_PST(b0);
 #if VB_PRED_GATHER
     if constexpr (kBufs == 2) {
       if (t == 0) VB_WAIT_VMCNT(0);
@@ -585,10 +605,18 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     } else {
       if (t == 0) VB_WAIT_VMCNT(kInstPerWave);
       else VB_WAIT_VMCNT(kInstPerWave + kSt);
+      VB_PST(b1);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      VB_PST(b2);
       issue_idx(t + 3);
       issue(t + 2);
+      VB_PST(b3);
+#if VB_PRED_STAMPS
+      pst[0] += b1 - b0;
+      pst[1] += b2 - b1;
+      pst[2] += b3 - b2;
+#endif
     }
 #else
     // retire this wave's DMA of tile t, then the barrier makes every wave's part visible and
@@ -662,6 +690,10 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     // hardware drops those lanes.
 #pragma unroll
     for (int pr = 0; pr < kSt; ++pr) store16(rsrd, (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
+#if VB_PRED_STAMPS
+    VB_PST(b4);
+    pst[3] += b4 - b0;
+#endif
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
     body(t0, std::integral_constant<int, 0>{});
@@ -674,6 +706,9 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
   static_assert(kBufs >= 2 && kBufs <= 4, "the loop body is instantiated once per ring slot");
 #if VB_PRED_GATHER
   VB_WAIT_VMCNT(0);   // the DMAs issued past the last tile land before the epilogue reuses the LDS
+#endif
+#if VB_PRED_STAMPS
+  VB_PST(e0);
 #endif
   m = max_xor32(m);   // the two halves saw alternate key blocks
   if (half == 0) mrow_s[wave * 32 + l32] = m;
@@ -733,6 +768,16 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     val[j] = v;
     po[j] = T::from_f32(v);
   }
+#if VB_PRED_STAMPS
+  {
+    VB_PST(e1);
+    if (lane == 0) {
+      for (int i = 0; i < 4; ++i) atomicAdd(&g_pred_stamp[i], pst[i]);
+      atomicAdd(&g_pred_stamp[4], e1 - e0);
+      atomicAdd(&g_pred_stamp[5], 1ull);
+    }
+  }
+#endif
   if (!kEnergy || p.mask == nullptr) return;   // scores only (energy rule elsewhere / not wanted)
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
@@ -821,6 +866,15 @@ static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t st
 }
 
 }  // namespace vb
+
+#if VB_PRED_STAMPS
+// diagnostic builds only: read and clear the score kernel's phase sums
+extern "C" int vb_debug_pred_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vb::g_pred_stamp), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(vb::g_pred_stamp), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" uint64_t vb_mask_predict_workspace_size(const vb_predict_args* a) {
   if (!a || a->B <= 0 || a->H <= 0 || a->L <= 0 || a->D <= 0) return 0;
