@@ -52,7 +52,10 @@ template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
 #ifndef VB_PRED_MIN_WG
 #define VB_PRED_MIN_WG 2
 #endif
-template <int D> constexpr int kPBufs = VB_PRED_BUFS;
+#ifndef VB_PRED_BUFS64
+#define VB_PRED_BUFS64 2   // D=64: a 2-slot ring (36.5 KiB of LDS, four workgroups per CU), see kFusedPoolWgs64
+#endif
+template <int D> constexpr int kPBufs = D == 64 ? VB_PRED_BUFS64 : VB_PRED_BUFS;
 #ifndef VB_PRED_GATHER
 #define VB_PRED_GATHER 1   // K rows gathered by the score kernel's DMA (no sampled-row copy)
 #endif
@@ -64,6 +67,13 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 #define VB_FUSED_POOL_WGS 512   // workgroups of the predictor's launch that run the pooled K/V pass
 #endif
 constexpr int kFusedPoolWgs = VB_FUSED_POOL_WGS;
+#ifndef VB_FUSED_POOL_WGS64
+// D=64 (CogVideoX): with four score workgroups per CU, 384 pooling workgroups leave more slots to the
+// score workgroups while the pass runs (per call 1.006x against the 3-slot ring with 512; 512 with
+// the 2-slot ring 0.97x, 256 0.99x; Wan keeps the 3-slot ring and 512: 0.98x with 2 slots + 384)
+#define VB_FUSED_POOL_WGS64 384
+#endif
+constexpr int kFusedPoolWgs64 = VB_FUSED_POOL_WGS64;
 
 // multi-level rank bands (value, [start, end) in ranks) for the fused level-mask epilogue
 struct PredBands {
@@ -956,7 +966,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
     t.k_r = reinterpret_cast<uint8_t*>(a->pool_k_r); t.v_r = reinterpret_cast<uint8_t*>(a->pool_v_r);
     const int64_t items = (int64_t)a->B * a->H * t.Lp * (a->D / 8);
     int n = (int)((items + 255) / 256);
-    n = n < kFusedPoolWgs ? n : kFusedPoolWgs;
+    const int cap = a->D == 64 ? kFusedPoolWgs64 : kFusedPoolWgs;
+    n = n < cap ? n : cap;
     p.n_pool = (n + 7) / 8 * 8;   // keeps blockIdx % 8 of the score workgroups (their XCD)
   }
   if (a->pyr_k) {   // the KV pyramid pass rides in the score kernel's launch
@@ -974,7 +985,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
     t.kpyr = reinterpret_cast<uint8_t*>(a->pyr_k); t.vpyr = reinterpret_cast<uint8_t*>(a->pyr_v);
     const int64_t items = (int64_t)a->B * a->H * (t.Lpad / 8) * (a->D / 8);
     int n = (int)((items + 255) / 256);
-    n = n < kFusedPoolWgs ? n : kFusedPoolWgs;
+    const int cap = a->D == 64 ? kFusedPoolWgs64 : kFusedPoolWgs;
+    n = n < cap ? n : cap;
     p.n_pool = (n + 7) / 8 * 8;   // keeps blockIdx % 8 of the score workgroups (their XCD)
     p.pool_kind = 2;
   }
