@@ -32,7 +32,8 @@ constexpr int kPThreads = 64 * kPWaves;
 constexpr int kMaxNb = 320;        // sampled blocks per side (L <= 40960 at block 128)
 constexpr int kEnergyRow = kMaxNb + 16;   // LDS floats per energy-rule row buffer (keys padded to 16)
 // keys per LDS tile: D=64 streams four 32-key sampled blocks per barrier (16 MFMAs per wave),
-// D=128 two (also 16 MFMAs); a 3-deep ring keeps the LDS at 48 KiB (3 workgroups per CU)
+// D=128 two (also 16 MFMAs); 16 KiB tiles in a 2-deep ring at D=64 (36.5 KiB with the row-offset
+// ring: four workgroups per CU) and a 3-deep ring at D=128 (52.5 KiB: three per CU)
 template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
 #ifndef VB_PRED_BUFS
 #define VB_PRED_BUFS 3
