@@ -388,6 +388,38 @@ def test_philox_claim_declines_draws_past_one_pass():
     assert ops.claim_rand_draws(DEV, ops.RAND_ONE_PASS_NUMEL + 128) is None
 
 
+def test_module_call_captures_into_a_hip_graph_with_torch_rand_draws():
+    """Under HIP-graph capture the module keeps torch.rand (graph-safe per-replay offsets) instead of
+    the in-kernel draws, and a captured call replays: finite outputs of the right shape, and the
+    graph's outputs equal an eager call's given the same mask."""
+    import vblade
+    from vblade import ops
+    m = vblade.AdaptiveBlockSparseAttn("cog", log_every=0, width=8, height=6, depth=10,
+                                       text_length=30, min_retain_ratio=0.2, max_retain_ratio=0.5)
+    B, H, L, D = 1, 2, m.gilbert_rearranger.seq_len, 64
+    g = torch.Generator().manual_seed(77)
+    q, k, v = (torch.randn(B, H, L, D, generator=g).bfloat16().to(DEV) for _ in range(3))
+    with torch.no_grad():
+        m(q, k, v)                                   # warm up outside the capture
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                assert ops.claim_rand_draws(DEV, B * H * 128) is None
+                out = m(q, k, v)
+        torch.cuda.current_stream().wait_stream(s)
+        for _ in range(2):
+            graph.replay()
+        torch.cuda.synchronize()
+        assert out.shape == q.shape and bool(torch.isfinite(out.float()).all())
+        mask = m.last_mask.clone()
+        eager = m(q, k, v, block_mask=mask)
+        torch.cuda.synchronize()
+        assert (eager.float() - out.float()).abs().max().item() <= 2.5e-2
+
+
 @pytest.mark.parametrize("n,keep", [(128, 32), (131, 32), (61, 7), (256, 256)])
 def test_sample_offsets_ties_and_ragged_row_lengths(n, keep):
     """The rank loop reads four draws per LDS broadcast with a scalar tail: rows whose length is

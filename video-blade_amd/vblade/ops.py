@@ -385,8 +385,13 @@ PHILOX_DRAWS = os.environ.get("VB_PHILOX_DRAWS", "1") != "0"   # off: the caller
 def claim_rand_draws(device, numel: int, draws: int = 2):
     """Reserve ``draws`` consecutive torch.rand(numel) calls on ``device``'s default generator for
     a kernel that generates them itself: returns (seed, offset) and advances the generator's offset
-    as those calls would, or None when the draw is too large for one pass (then call torch.rand)."""
+    as those calls would, or None when the draw is too large for one pass or the stream is being
+    captured into a graph (then call torch.rand)."""
     if numel > RAND_ONE_PASS_NUMEL or not PHILOX_DRAWS:
+        return None
+    # under HIP-graph capture torch.rand draws from a per-replay offset; a seed/offset read here
+    # would be baked into the graph, so captured calls keep torch.rand
+    if torch.cuda.is_current_stream_capturing():
         return None
     dev = torch.device(device)
     gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
