@@ -29,7 +29,8 @@ struct FwdParams {
 #define VB_DIAG 0
 #endif
 #ifndef VB_VPRE64
-#define VB_VPRE64 3   // V^T k-steps prefetched before the softmax (D=64); 4 spills the lazy-max loop
+#define VB_VPRE64 4   // V^T k-steps prefetched before the softmax (D=64); 4 under the iterative-ilp scheduler
+                      // (attention kernel 1.016-1.030x on three boxes, bit-identical; 3 was best before it)
 #endif
 #ifndef VB_MFMA_ROWSUM
 #define VB_MFMA_ROWSUM 0
