@@ -33,7 +33,9 @@ def fwd_asm(tmp_path_factory):
     out = tmp_path_factory.mktemp("asm") / "fwd.s"
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "video-blade_amd", "csrc"),
-           "-fno-slp-vectorize", "-fno-honor-nans", "--cuda-device-only", "-S", SRC, "-o", str(out)]
+           # the Makefile's flags for this file (video-blade_amd/Makefile)
+           "-fno-slp-vectorize", "-fno-honor-nans", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp",
+           "--cuda-device-only", "-S", SRC, "-o", str(out)]
     subprocess.run(cmd, check=True, capture_output=True)
     return out.read_text()
 

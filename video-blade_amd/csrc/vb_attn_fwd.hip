@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     }
     // V^T fragments (ds_read_b64_tr_b16) for the first VPRE k-steps, issued before the softmax
     // VALU so they land while it runs; the rest are fetched one k-step ahead inside the PV loop.
-    constexpr int VPRE = (D == 64 && !VB_MFMA_ROWSUM) ? VB_VPRE64 : 2;
+    constexpr int VPRE = (D == 64 && !VB_MFMA_ROWSUM) ? (kKvRows ? VB_VPRE64_ROWS : VB_VPRE64) : 2;
     s16x4 vlo[4][DT], vhi[4][DT];
     auto read_v = [&](int kk) __attribute__((always_inline)) {
       const int row0 = (kk >> 1) * 32 + 16 * (kk & 1);   // + vrow (in v_lane)

@@ -32,6 +32,10 @@ struct FwdParams {
 #define VB_VPRE64 4   // V^T k-steps prefetched before the softmax (D=64); 4 under the iterative-ilp scheduler
                       // (attention kernel 1.016-1.030x on three boxes, bit-identical; 3 was best before it)
 #endif
+#ifndef VB_VPRE64_ROWS
+#define VB_VPRE64_ROWS 3   // the same for the launches that gather K/V rows through the Gilbert index:
+                           // 4 spills a DMA offset into their tile-issue blocks (tests/test_codegen.py)
+#endif
 #ifndef VB_MFMA_ROWSUM
 #define VB_MFMA_ROWSUM 0
 #endif
