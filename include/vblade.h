@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VB_ABI_VERSION 1
+#define VB_ABI_VERSION 2   /* 2: mask_head_mode argument of vb_block_sparse_attn_fwd/bwd */
 
 enum vb_status {
   VB_OK = 0,
@@ -33,6 +33,8 @@ enum vb_status {
 };
 
 enum vb_dtype { VB_DTYPE_BF16 = 0, VB_DTYPE_F16 = 1 };
+/* reading of head_mask_type = ones(H) (see vb_block_sparse_attn_fwd) */
+enum vb_mask_head_mode { VB_MASK_HEAD_PER_HEAD = 0, VB_MASK_HEAD_SHARED0 = 1 };
 
 /* Message of the last failing call on this thread ("" if none). */
 const char* vb_last_error(void);
@@ -52,9 +54,13 @@ int vb_gilbert3d_perm(int width, int height, int depth, int32_t* perm_out);
  * call; wanx_blocksparseattn.py:301-305).
  *   q/k/v_unpad   [total, H, D] contiguous, dtype `dtype`
  *   cu_seqlens_*  int32 [batch+1] (device)
- *   head_mask_type int32 [H] (device): 0 dense; m>0 block-sparse with base_blockmask head m-1,
- *                 where every 1 is first renumbered 1,2,3,... in head order (the library's
- *                 replace_ones_with_count); m<0 (streaming) -> that head's output is NaN.
+ *   head_mask_type int32 [H] (device): 0 dense; m>0 block-sparse with base_blockmask head m-1;
+ *                 m<0 (streaming) -> that head's output is NaN. How the reference's
+ *                 head_mask_type = ones(H) (cog :313) reads is open offline:
+ *                 mask_head_mode VB_MASK_HEAD_PER_HEAD (0, default) first renumbers every 1 to
+ *                 1,2,3,... in head order (Block-Sparse-Attention's replace_ones_with_count: one
+ *                 predicted mask per head); VB_MASK_HEAD_SHARED0 (1) reads m literally, so ones(H)
+ *                 gives every head base_blockmask head 0.
  *   streaming_info ignored (only used by streaming heads)
  *   base_blockmask uint8/bool [batch, n_sparse, ceil(max_q/128), ceil(max_k/128)] contiguous
  *   out_unpad     [total_q, H, D]; softmax_lse fp32 [batch, H, max_seqlen_q] (natural log).
@@ -71,7 +77,7 @@ int vb_block_sparse_attn_fwd(const void* q_unpad, const void* k_unpad, const voi
                              const uint8_t* base_blockmask, int batch, int num_heads, int head_dim,
                              int max_seqlen_q, int max_seqlen_k, float p_dropout, int deterministic,
                              float softmax_scale, int is_causal, int exact_streaming, int dtype,
-                             void* out_unpad, float* softmax_lse, void* stream);
+                             void* out_unpad, float* softmax_lse, int mask_head_mode, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Native strided block-sparse attention forward (the adaptive module's hot kernel). One softmax
@@ -158,7 +164,9 @@ typedef struct vb_predict_args {
    * generator at state (philox_seed, philox_offset): element i of a draw = the x value of the first
    * hiprand_uniform4 of Philox4x32-10 subsequence i (1.0 mapped to 0.0), the q draw at
    * philox_offset and the k draw at philox_offset + 4 (each torch.rand call advances the offset by
-   * 4 while B*H*block <= 524288, i.e. one pass of its grid-stride launch). The offsets are WRITTEN
+   * 4 per call). Element i takes the x of thread i only while every element has a thread of its own
+   * in torch.rand's grid-stride launch: B*H*block <= CUs x max threads per CU of the device (524288
+   * on an unpartitioned MI355X); past that the call fails with VB_ERR_UNSUPPORTED. The offsets are WRITTEN
    * to q_off/k_off; the caller advances its generator by 8. */
   int philox;
   uint64_t philox_seed;
@@ -268,7 +276,7 @@ int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, const void* 
                              int max_seqlen_q, int max_seqlen_k, float p_dropout, float softmax_scale,
                              int is_causal, int exact_streaming, int deterministic, int dtype,
                              void* dq, void* dk, void* dv, void* workspace, uint64_t workspace_bytes,
-                             void* stream);
+                             int mask_head_mode, void* stream);
 
 /* ==========================================================================================
  * Multi-level block-sparse attention: the VBench sampler's op (cogvideox/sample_evaluate/

@@ -13,5 +13,19 @@ for p in (os.path.join(ROOT, "video-blade_amd"), os.path.join(ROOT, "oracle"), R
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+# name -> list of facts recorded by tests and printed in the terminal summary (e.g. how many of the
+# reference-golden cases reproduced the reference's mask bit for bit)
+RECORD = {}
+
+
+def record(name, fact):
+    RECORD.setdefault(name, []).append(fact)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) and libvblade_hip.so")
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    for name, facts in RECORD.items():
+        terminalreporter.write_line(f"[vblade record] {name}: {facts}")

@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.vb_abi_version() == 1
+    assert lib.vb_abi_version() == 2
 
 
 def test_struct_layouts_match_header():
@@ -82,11 +82,15 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     assert b"positive" in lib.vb_last_error()
     # dropout is rejected before any device work
     rc = lib.vb_block_sparse_attn_fwd(1, 1, 1, 1, 1, None, None, None, 1, 1, 64, 128, 128,
-                                      0.1, 1, 0.0, 0, 0, 0, 1, 1, None)
+                                      0.1, 1, 0.0, 0, 0, 0, 1, 1, 0, None)
     assert rc == _lib.VB_ERR_UNSUPPORTED and b"dropout" in lib.vb_last_error()
     rc = lib.vb_block_sparse_attn_fwd(1, 1, 1, 1, 1, None, None, None, 1, 1, 64, 128, 128,
-                                      0.0, 1, 0.0, 1, 0, 0, 1, 1, None)
+                                      0.0, 1, 0.0, 1, 0, 0, 1, 1, 0, None)
     assert rc == _lib.VB_ERR_UNSUPPORTED
+    # SURVEY Appendix B's mask_head_mode: per_head (0) and shared_head0 (1) only
+    rc = lib.vb_block_sparse_attn_fwd(1, 1, 1, 1, 1, None, None, None, 1, 1, 64, 128, 128,
+                                      0.0, 1, 0.0, 0, 0, 0, 1, 1, 2, None)
+    assert rc == _lib.VB_ERR_INVALID and b"mask_head_mode" in lib.vb_last_error()
     a = _lib.AttnArgs()
     assert lib.vb_attn_fwd(ctypes.byref(a), None) == _lib.VB_ERR_INVALID
     p = _lib.PredictArgs()
@@ -106,8 +110,11 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     assert lib.vb_attn_bwd_workspace_size(ctypes.byref(b)) >= 2 * 64 * 4 * 4
     assert lib.vb_block_sparse_attn_bwd_workspace_size(1, 1, 128) > 0
     rc = lib.vb_block_sparse_attn_bwd(*([None] * 11), 1, 1, 64, 128, 128, 0.1, 0.0, 0, 0, 1, 0,
-                                      None, None, None, None, 0, None)
+                                      None, None, None, None, 0, 0, None)
     assert rc == _lib.VB_ERR_UNSUPPORTED and b"dropout" in lib.vb_last_error()
+    rc = lib.vb_block_sparse_attn_bwd(*([None] * 11), 1, 1, 64, 128, 128, 0.0, 0.0, 0, 0, 1, 0,
+                                      None, None, None, None, 0, 5, None)
+    assert rc == _lib.VB_ERR_INVALID and b"mask_head_mode" in lib.vb_last_error()
     # multi-level entry points
     assert lib.vb_kv_pyramid_rows(17776) == 15 * 17792 // 8
     assert lib.vb_kv_pyramid_rows(128) == 240
@@ -149,10 +156,16 @@ def test_mask_predict_option_checks_without_gpu(lib):
     p.philox, p.rand_q, p.rand_k = 1, 1 << 20, 1 << 20
     assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
     assert b"exclusive" in lib.vb_last_error()
-    p = args(B=2, H=2049)                         # 2*2049*128 > 524288
+    p = args(B=2, H=2049)                         # 2*2049*128 > 524288 (CUs x threads per CU)
     p.philox = 1
-    assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_UNSUPPORTED
-    assert b"524288" in lib.vb_last_error()
+    rc = lib.vb_mask_predict(ctypes.byref(p), None)
+    import torch
+    if torch.cuda.is_available():   # the bound is the device's own CUs x max threads per CU
+        pr = torch.cuda.get_device_properties(0)
+        assert rc == _lib.VB_ERR_UNSUPPORTED
+        assert str(pr.multi_processor_count * pr.max_threads_per_multi_processor).encode() in lib.vb_last_error()
+    else:                           # no device to query: refused before any launch
+        assert rc == _lib.VB_ERR_LAUNCH and b"CU count" in lib.vb_last_error()
     vals = np.array([3], dtype=np.int32)
     se = np.array([0.0, 1.0], dtype=np.float64)
     p = args()

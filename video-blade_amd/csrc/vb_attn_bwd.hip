@@ -62,6 +62,7 @@ struct BwdParams {
   const void* kp; const void* vp; int64_t kps[3], vps[3];
   int Lkp;
   const int32_t* cu_q; const int32_t* cu_k; const int32_t* head_mask_type;
+  int hm_mode;   // VB_MASK_HEAD_PER_HEAD / VB_MASK_HEAD_SHARED0 (head_mask_base)
   const uint8_t* mask; int64_t ms[3];
   const float* stats; int ntile;
   void* dq; int64_t dqs[3]; const int32_t* q_rows;
@@ -284,7 +285,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   bool nan_head = false;
   const uint8_t* mcol = nullptr;
   if (!kPooled || kML) {
-    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head, p.hm_mode);
     if (mh) mcol = mh + (kML ? (ml_m << ml_e) : kblk);
   }
   const int qlo = (kPooled && !kML) ? split * nbq / p.psplit : 0;
@@ -719,7 +720,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
   const uint8_t* mrow = nullptr;
   const bool use_main = p.k != nullptr;
   if (use_main) {
-    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head, p.hm_mode);
     if (mh) mrow = mh + (int64_t)qblk * p.ms[2];
   }
   if (kML) {
@@ -1261,12 +1262,14 @@ extern "C" int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, c
                                         int max_seqlen_q, int max_seqlen_k, float p_dropout, float softmax_scale,
                                         int is_causal, int exact_streaming, int deterministic, int dtype,
                                         void* dq, void* dk, void* dv, void* workspace, uint64_t workspace_bytes,
-                                        void* stream) {
+                                        int mask_head_mode, void* stream) {
   using namespace vb;
   (void)streaming_info;
   (void)deterministic;  // always deterministic (no atomics)
   if (p_dropout != 0.f) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: p_dropout must be 0");
   if (is_causal || exact_streaming) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_bwd: causal/streaming not supported");
+  if (mask_head_mode != VB_MASK_HEAD_PER_HEAD && mask_head_mode != VB_MASK_HEAD_SHARED0)
+    return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: unknown mask_head_mode");
   if (!dout || !q_unpad || !k_unpad || !v_unpad || !out_unpad || !softmax_lse || !cu_seqlens_q || !cu_seqlens_k ||
       !dq || !dk || !dv)
     return fail(VB_ERR_INVALID, "vb_block_sparse_attn_bwd: null tensor");
@@ -1303,6 +1306,7 @@ extern "C" int vb_block_sparse_attn_bwd(const void* dout, const void* q_unpad, c
   p.q = q_unpad; p.dout = dout; p.k = k_unpad; p.v = v_unpad;
   for (int i = 0; i < 3; ++i) p.qs[i] = p.dos[i] = p.ks[i] = p.vs[i] = p.dqs[i] = p.dks[i] = p.dvs[i] = s3[i];
   p.cu_q = cu_seqlens_q; p.cu_k = cu_seqlens_k; p.head_mask_type = head_mask_type;
+  p.hm_mode = mask_head_mode;
   p.mask = base_blockmask;
   p.ms[0] = head_mask_type ? -1 : (int64_t)num_heads * nbq * nbk;
   p.ms[1] = (int64_t)nbq * nbk; p.ms[2] = nbk;

@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   bool dense = true;
   bool nan_head = false;
   if (p.use_main) {
-    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head);
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head, p.hm_mode);
     if (mh) {
       dense = false;
       mrow = mh + (int64_t)qblk * p.ms[2];
@@ -1115,12 +1115,14 @@ extern "C" int vb_block_sparse_attn_fwd(const void* q_unpad, const void* k_unpad
                                         const uint8_t* base_blockmask, int batch, int num_heads, int head_dim,
                                         int max_seqlen_q, int max_seqlen_k, float p_dropout, int deterministic,
                                         float softmax_scale, int is_causal, int exact_streaming, int dtype,
-                                        void* out_unpad, float* softmax_lse, void* stream) {
+                                        void* out_unpad, float* softmax_lse, int mask_head_mode, void* stream) {
   using namespace vb;
   (void)streaming_info;
   (void)deterministic;
   if (p_dropout != 0.f) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_fwd: p_dropout must be 0");
   if (is_causal || exact_streaming) return fail(VB_ERR_UNSUPPORTED, "vb_block_sparse_attn_fwd: causal/streaming not supported");
+  if (mask_head_mode != VB_MASK_HEAD_PER_HEAD && mask_head_mode != VB_MASK_HEAD_SHARED0)
+    return fail(VB_ERR_INVALID, "vb_block_sparse_attn_fwd: unknown mask_head_mode");
   if (!q_unpad || !k_unpad || !v_unpad || !cu_seqlens_q || !cu_seqlens_k || !out_unpad)
     return fail(VB_ERR_INVALID, "vb_block_sparse_attn_fwd: null tensor");
   if (batch <= 0 || num_heads <= 0 || max_seqlen_q <= 0 || max_seqlen_k <= 0)
@@ -1138,6 +1140,7 @@ extern "C" int vb_block_sparse_attn_fwd(const void* q_unpad, const void* k_unpad
   p.qs[2] = p.ks[2] = p.vs[2] = p.os[2] = row;
   p.cu_q = cu_seqlens_q; p.cu_k = cu_seqlens_k;
   p.head_mask_type = head_mask_type;
+  p.hm_mode = mask_head_mode;
   p.use_main = 1;
   p.mask = base_blockmask;  // may be NULL: dense
   // base_blockmask [batch, n_sparse, nbq, nbk]: n_sparse (= number of heads whose mask id is 1) is

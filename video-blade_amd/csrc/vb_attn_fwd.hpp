@@ -10,6 +10,7 @@ struct FwdParams {
   const int32_t* q_rows; const int32_t* kv_rows;
   const int32_t* cu_q; const int32_t* cu_k;   // varlen row offsets (reference API), nullable
   const int32_t* head_mask_type;              // reference API, nullable
+  int hm_mode;                                // VB_MASK_HEAD_PER_HEAD / VB_MASK_HEAD_SHARED0
   int use_main;
   const uint8_t* mask; int64_t ms[3];
   const void* kp; const void* vp; int64_t kps[3], vps[3];

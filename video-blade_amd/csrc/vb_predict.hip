@@ -853,6 +853,21 @@ static uint64_t predict_ws_bytes(int B, int H, int L, int D) {
   return predict_rows_bytes(B, H, L, D) + (uint64_t)B * H * nb * nb * 32 * 2;
 }
 
+// B*H*block bound of the in-kernel Philox draws (see vb_mask_predict), per device, cached
+static int64_t philox_x_only_numel() {
+  static int64_t cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+  if (dev < 64 && cache[dev] > 0) return cache[dev];
+  int cus = 0, thr = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&thr, hipDeviceAttributeMaxThreadsPerMultiProcessor, dev) != hipSuccess)
+    return 0;
+  const int64_t n = (int64_t)cus * thr;
+  if (dev < 64) cache[dev] = n;
+  return n;
+}
+
 template <int D, class T>
 static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t staged) {
   const size_t smem = predict_smem_bytes(p.nb, D);
@@ -934,6 +949,8 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
     return fail(VB_ERR_INVALID, "vb_mask_predict: 0..8 level bands with value/start/end arrays");
   if (a->mask_level) {
     if (!a->mask) return fail(VB_ERR_INVALID, "vb_mask_predict: mask_level needs a mask output");
+    if (VB_PRED_SPLIT_ENERGY)   // that diagnostic build's epilogue writes the energy mask only
+      return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: mask_level needs the fused epilogue (VB_PRED_SPLIT_ENERGY=0)");
     p.level = 1;
     p.lv.n = a->level_bands;
     for (int i = 0; i < a->level_bands; ++i) {
@@ -949,8 +966,14 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   }
   if (a->philox) {
     if (a->rand_q || a->rand_k) return fail(VB_ERR_INVALID, "vb_mask_predict: philox and rand_q/rand_k are exclusive");
-    if ((int64_t)a->B * a->H * a->block > 524288)
-      return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: philox draws need B*H*block <= 524288");
+    // torch.rand's grid-stride launch gives element i the x value of thread i only while every
+    // element has a thread of its own: numel <= CUs * max threads per CU of THIS device (524288 on
+    // an unpartitioned MI355X; fewer in a CPX partition)
+    const int64_t one_pass = philox_x_only_numel();
+    if (one_pass <= 0) return fail(VB_ERR_LAUNCH, "vb_mask_predict: cannot query the device's CU count");
+    if ((int64_t)a->B * a->H * a->block > one_pass)
+      return fail(VB_ERR_UNSUPPORTED, "vb_mask_predict: philox draws need B*H*block <= " + std::to_string(one_pass) +
+                                          " (CUs x max threads per CU of this device)");
     p.philox = 1; p.philox_seed = a->philox_seed; p.philox_offset = a->philox_offset;
   }
   if (a->pool_kp) {   // the pooled K/V pass rides in the score kernel's launch

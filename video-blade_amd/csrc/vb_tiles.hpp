@@ -149,12 +149,15 @@ __device__ __forceinline__ int tr_col(int lane) { return 16 * ((lane >> 4) & 1) 
 
 // ---- reference-API block-mask addressing ----------------------------------------------------------
 // Block-Sparse-Attention's head_mask_type: 0 dense; m > 0 block-sparse with base_blockmask head
-// m-1 after every 1 is renumbered 1,2,3.. in head order (its replace_ones_with_count); m < 0 a
-// streaming head (unsupported: NaN output). ms[0] < 0 = batch stride counted on the device as
-// (#heads with id 1) * ms[1]. Returns the (b, h) mask base (row 0, column 0) or nullptr if dense.
+// m-1; m < 0 a streaming head (unsupported: NaN output). `mode` (open offline):
+// VB_MASK_HEAD_PER_HEAD renumbers every 1 to 1,2,3.. in head order first (the library's
+// replace_ones_with_count: ones(H) -> one mask per head); VB_MASK_HEAD_SHARED0 reads m literally
+// (ones(H) -> every head uses base_blockmask head 0). ms[0] < 0 = batch stride counted on the
+// device as (#heads with id 1) * ms[1]. Returns the (b, h) mask base (row 0, column 0) or nullptr
+// if dense.
 __device__ __forceinline__ const uint8_t* head_mask_base(const uint8_t* mask, const int64_t* ms,
                                                          const int32_t* hmt, int H, int b, int h,
-                                                         bool& nan_head) {
+                                                         bool& nan_head, int mode = VB_MASK_HEAD_PER_HEAD) {
   nan_head = false;
   if (mask == nullptr) return nullptr;
   int mh = h;
@@ -162,7 +165,7 @@ __device__ __forceinline__ const uint8_t* head_mask_base(const uint8_t* mask, co
     const int t = hmt[h];
     if (t == 0) return nullptr;
     if (t < 0) { nan_head = true; return nullptr; }
-    if (t == 1) {
+    if (t == 1 && mode == VB_MASK_HEAD_PER_HEAD) {
       int cnt = 0;
       for (int i = 0; i <= h; ++i) cnt += (hmt[i] == 1);
       mh = cnt - 1;

@@ -137,7 +137,7 @@ SIGNATURES = {
         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_float, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-        _vp, _vp, _vp]),
+        _vp, _vp, ctypes.c_int, _vp]),
     "vb_attn_fwd": (ctypes.c_int, [ctypes.POINTER(AttnArgs), _vp]),
     "vb_mask_predict_workspace_size": (ctypes.c_uint64, [ctypes.POINTER(PredictArgs)]),
     "vb_mask_predict": (ctypes.c_int, [ctypes.POINTER(PredictArgs), _vp]),
@@ -155,7 +155,7 @@ SIGNATURES = {
         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
         ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-        _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+        _vp, _vp, _vp, _vp, ctypes.c_uint64, ctypes.c_int, _vp]),
     "vb_kv_pyramid_rows": (ctypes.c_int, [ctypes.c_int]),
     "vb_kv_pyramid": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -192,7 +192,7 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.vb_abi_version() != 1:
+    if lib.vb_abi_version() != 2:
         raise VBladeError("libvblade_hip.so ABI version mismatch")
     _lib = lib
     return lib

@@ -109,6 +109,11 @@ class AdaptiveBlockSparseAttn(nn.Module):
     (Wan2.1-1.3B). Keyword arguments override the reference's module globals.
     combine: "fused" (one softmax, inference default) or "reference" (two attention calls + the
     reference's bf16 LSE combine, bit-for-bit structure of :366-393; always used under autograd).
+    mask_head_mode: how the reference's head_mask_type = ones(H) (:313) reads the predicted
+    [B,H,nb,nb] mask, which SURVEY Appendix B leaves open offline: "per_head" (default: each head
+    its own predicted mask, Block-Sparse-Attention's renumbering of the ones) or "shared_head0"
+    (every head attends with head 0's mask). The sparsity statistic counts the predicted mask in
+    both modes, as the reference's (:394) does.
     """
 
     def __init__(self, variant: str = "cog", *, combine: str = "fused", **overrides):
@@ -116,7 +121,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
         if variant not in VARIANT_DEFAULTS:
             raise ValueError(f"variant must be one of {list(VARIANT_DEFAULTS)}")
         cfg = dict(VARIANT_DEFAULTS[variant])
-        unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep", "overlap", "gather_kv"}
+        unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep", "overlap", "gather_kv",
+                                               "mask_head_mode"}
         if unknown:
             raise TypeError(f"unknown options {sorted(unknown)}")
         cfg.update(overrides)
@@ -134,6 +140,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
         if self.block != 128 or self.num_keep != 32:
             raise ValueError("block=128 and num_keep=32 are the reference's (only) values")
         self.log_every = int(cfg["log_every"])
+        self.mask_head_mode = cfg.get("mask_head_mode", "per_head")
+        ops.mask_head_mode_code(self.mask_head_mode)   # validates
         self.gilbert_rearranger = GilbertRearranger(cfg["width"], cfg["height"], cfg["depth"],
                                                     self.text_length)
         # running sparsity statistic kept on the device (the reference's .item() per call, :415,
@@ -270,6 +278,10 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self._slot_totals.append(B * H * nb * nb)
         self.sparsity_counter += 1
         self.last_mask = mask
+        if self.mask_head_mode == "shared_head0":
+            # head_mask_type's ones read literally: every head uses base_blockmask head 0 (a
+            # head-stride-0 view; the kernels index the mask through its strides)
+            mask = mask[:, :1].expand(B, H, mask.shape[2], mask.shape[3])
         if not fused:
             from .autograd import adaptive_split_attention
             out = adaptive_split_attention(q, k, v, mask, rows, self.sample_gap,

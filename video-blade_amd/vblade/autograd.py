@@ -18,34 +18,38 @@ from . import ops
 class _BlockSparseAttnFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, cu_q, cu_k, head_mask_type, streaming_info, base_blockmask,
-                max_q, max_k, p_dropout, deterministic, softmax_scale, is_causal, exact_streaming):
+                max_q, max_k, p_dropout, deterministic, softmax_scale, is_causal, exact_streaming,
+                mask_head_mode):
         out, lse = ops.block_sparse_attn_fwd(q, k, v, cu_q, cu_k, head_mask_type, streaming_info,
                                              base_blockmask, max_q, max_k, p_dropout,
                                              deterministic, softmax_scale, is_causal,
-                                             exact_streaming)
+                                             exact_streaming, mask_head_mode=mask_head_mode)
         ctx.save_for_backward(q, k, v, out, lse, cu_q, cu_k, head_mask_type, base_blockmask)
-        ctx.meta = (max_q, max_k, softmax_scale)
+        ctx.meta = (max_q, max_k, softmax_scale, mask_head_mode)
         ctx.mark_non_differentiable(lse)
         return out, lse
 
     @staticmethod
     def backward(ctx, dout, _dlse):
         q, k, v, out, lse, cu_q, cu_k, hmt, mask = ctx.saved_tensors
-        max_q, max_k, scale = ctx.meta
+        max_q, max_k, scale, mode = ctx.meta
         dq, dk, dv = ops.block_sparse_attn_bwd(dout, q, k, v, out, lse, cu_q, cu_k, hmt, None,
-                                               mask, max_q, max_k, softmax_scale=scale)
-        return (dq, dk, dv) + (None,) * 12
+                                               mask, max_q, max_k, softmax_scale=scale,
+                                               mask_head_mode=mode)
+        return (dq, dk, dv) + (None,) * 13
 
 
 def block_sparse_attn_func(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k, head_mask_type,
                            streaming_info, base_blockmask, max_seqlen_q_, max_seqlen_k_, p_dropout,
                            deterministic=False, softmax_scale=None, is_causal=False,
-                           exact_streaming=False, return_attn_probs=False):
-    """Same signature and return convention as the reference's external op."""
+                           exact_streaming=False, return_attn_probs=False, mask_head_mode="per_head"):
+    """Same signature and return convention as the reference's external op. ``mask_head_mode``
+    (keyword, not in the reference's signature): the reading of head_mask_type's ones that SURVEY
+    Appendix B leaves open offline ("per_head" default, "shared_head0")."""
     out, lse = _BlockSparseAttnFunc.apply(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k,
                                           head_mask_type, streaming_info, base_blockmask,
                                           max_seqlen_q_, max_seqlen_k_, p_dropout, deterministic,
-                                          softmax_scale, is_causal, exact_streaming)
+                                          softmax_scale, is_causal, exact_streaming, mask_head_mode)
     if return_attn_probs:
         return out, lse, None
     return out

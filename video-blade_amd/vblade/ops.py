@@ -141,12 +141,24 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
     return (out, lse) if need_lse else out
 
 
+MASK_HEAD_MODES = {"per_head": 0, "shared_head0": 1}   # vb_mask_head_mode
+
+
+def mask_head_mode_code(mode: str) -> int:
+    if mode not in MASK_HEAD_MODES:
+        raise ValueError(f"mask_head_mode must be one of {sorted(MASK_HEAD_MODES)}, got {mode!r}")
+    return MASK_HEAD_MODES[mode]
+
+
 def block_sparse_attn_fwd(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k, head_mask_type,
                           streaming_info, base_blockmask, max_seqlen_q, max_seqlen_k,
                           p_dropout=0.0, deterministic=False, softmax_scale=None,
-                          is_causal=False, exact_streaming=False):
+                          is_causal=False, exact_streaming=False, mask_head_mode="per_head"):
     """Forward of block_sparse_attn_func through vb_block_sparse_attn_fwd (varlen layout).
-    Returns (out_unpad [total_q,H,D], softmax_lse fp32 [B,H,max_seqlen_q])."""
+    Returns (out_unpad [total_q,H,D], softmax_lse fp32 [B,H,max_seqlen_q]). ``mask_head_mode``:
+    how head_mask_type's ones address base_blockmask's heads ("per_head": renumbered 1..H, one
+    mask per head; "shared_head0": read literally, every such head uses mask head 0)."""
+    mode = mask_head_mode_code(mask_head_mode)
     dev = _require_gpu(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k, base_blockmask)
     q_unpad, k_unpad, v_unpad = q_unpad.contiguous(), k_unpad.contiguous(), v_unpad.contiguous()
     B = cu_seqlens_q.numel() - 1
@@ -170,7 +182,7 @@ def block_sparse_attn_fwd(q_unpad, k_unpad, v_unpad, cu_seqlens_q, cu_seqlens_k,
         int(max_seqlen_k), float(p_dropout), int(bool(deterministic)),
         float(softmax_scale) if softmax_scale else 0.0, int(bool(is_causal)),
         int(bool(exact_streaming)), _dtype_code(q_unpad), out.data_ptr(), lse.data_ptr(),
-        _stream(dev)), "vb_block_sparse_attn_fwd")
+        mode, _stream(dev)), "vb_block_sparse_attn_fwd")
     return out, lse
 
 
@@ -244,9 +256,11 @@ def attention_bwd(dout, q, k, v, out, lse, *, block_mask=None, q_rows=None, kv_r
 def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_lse, cu_seqlens_q,
                           cu_seqlens_k, head_mask_type, streaming_info, base_blockmask,
                           max_seqlen_q, max_seqlen_k, p_dropout=0.0, softmax_scale=None,
-                          is_causal=False, exact_streaming=False, deterministic=True):
+                          is_causal=False, exact_streaming=False, deterministic=True,
+                          mask_head_mode="per_head"):
     """Backward of block_sparse_attn_func (vb_block_sparse_attn_bwd, varlen layout).
-    Returns (dq, dk, dv) [total, H, D]."""
+    Returns (dq, dk, dv) [total, H, D]. ``mask_head_mode`` as block_sparse_attn_fwd."""
+    mode = mask_head_mode_code(mask_head_mode)
     dev = _require_gpu(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_lse, base_blockmask)
     dout, q_unpad, k_unpad, v_unpad, out_unpad = (t.contiguous() for t in
                                                   (dout, q_unpad, k_unpad, v_unpad, out_unpad))
@@ -274,7 +288,7 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
         _ptr(streaming_info), _ptr(mask), B, H, D, int(max_seqlen_q), int(max_seqlen_k),
         float(p_dropout), float(softmax_scale) if softmax_scale else 0.0, int(bool(is_causal)),
         int(bool(exact_streaming)), int(bool(deterministic)), _dtype_code(q_unpad),
-        dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(), nbytes, _stream(dev)),
+        dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), ws.data_ptr(), nbytes, mode, _stream(dev)),
         "vb_block_sparse_attn_bwd")
     return dq, dk, dv
 
@@ -301,6 +315,19 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     run the same way; ``outs`` = kv_pyramid_outputs(k). Excludes ``pool``.
     ``level=mask_ratios``: the returned mask is the multi-level rank-band mask (level_mask's rule
     on the scores, computed by the score kernel's epilogue) instead of the energy mask."""
+    try:
+        return _mask_predict(q, k, q_off, k_off, rows=rows, energy_threshold=energy_threshold,
+                             min_keep=min_keep, max_keep=max_keep, force_tail=force_tail, scale=scale,
+                             mask_count=mask_count, want_mask=want_mask, staged_event=staged_event,
+                             rand=rand, philox=philox, pool=pool, pyr=pyr, level=level)
+    except Exception:
+        if philox is not None:   # the claimed draws were not used: give them back to the generator
+            release_rand_draws(q.device, philox)
+        raise
+
+
+def _mask_predict(q, k, q_off, k_off, *, rows, energy_threshold, min_keep, max_keep, force_tail,
+                  scale, mask_count, want_mask, staged_event, rand, philox, pool, pyr, level):
     if k.shape != q.shape:
         raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
                          f"got k {tuple(k.shape)}")
@@ -375,19 +402,38 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     return po, mask
 
 
-# torch.rand's launch on ROCm (ATen/native/hip/DistributionTemplates.h): one grid-stride pass of
-# 256-thread blocks, 4 uniforms per thread, while numel <= 256 * (CUs * 2048 / 256) * 4; each call
-# then advances the generator's Philox offset by 4. 524288 = that bound at 256 CUs.
-RAND_ONE_PASS_NUMEL = 524288
+# torch.rand's launch on ROCm (ATen/native/hip/DistributionTemplates.h, calc_execution_policy and
+# distribution_elementwise_grid_stride_kernel): 256-thread blocks, grid = min(ceil(numel / 256),
+# CUs * maxThreadsPerMultiProcessor / 256); thread i draws one hiprand_uniform4 per pass and element
+# li = i + pass_stride * c takes component c. Element i is the x component of thread i exactly while
+# numel <= CUs * maxThreadsPerMultiProcessor (every element has a thread of its own; 524288 on an
+# unpartitioned MI355X, fewer on a partitioned device or a smaller GPU). Each call then advances the
+# generator's Philox offset by 4.
+RAND_ONE_PASS_NUMEL = 524288   # the MI355X value; rand_one_pass_numel(device) is the per-device bound
 PHILOX_DRAWS = os.environ.get("VB_PHILOX_DRAWS", "1") != "0"   # off: the callers use torch.rand
+_ONE_PASS = {}
+
+
+def rand_one_pass_numel(device) -> int:
+    """Largest torch.rand numel whose element i is the x of Philox subsequence i on ``device``."""
+    if not torch.cuda.is_available():
+        return 0
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    n = _ONE_PASS.get(idx)
+    if n is None:
+        pr = torch.cuda.get_device_properties(idx)
+        n = _ONE_PASS[idx] = int(pr.multi_processor_count) * int(pr.max_threads_per_multi_processor)
+    return n
 
 
 def claim_rand_draws(device, numel: int, draws: int = 2):
     """Reserve ``draws`` consecutive torch.rand(numel) calls on ``device``'s default generator for
     a kernel that generates them itself: returns (seed, offset) and advances the generator's offset
-    as those calls would, or None when the draw is too large for one pass or the stream is being
-    captured into a graph (then call torch.rand)."""
-    if numel > RAND_ONE_PASS_NUMEL or not PHILOX_DRAWS:
+    as those calls would, or None when the draw is too large for one x-only pass on this device or
+    the stream is being captured into a graph (then call torch.rand). mask_predict gives the draws
+    back (release_rand_draws) when it raises before its launch."""
+    if not PHILOX_DRAWS or numel > rand_one_pass_numel(device):
         return None
     # under HIP-graph capture torch.rand draws from a per-replay offset; a seed/offset read here
     # would be baked into the graph, so captured calls keep torch.rand
@@ -398,6 +444,15 @@ def claim_rand_draws(device, numel: int, draws: int = 2):
     seed, off = gen.initial_seed(), gen.get_offset()
     gen.set_offset(off + 4 * draws)
     return seed, off
+
+
+def release_rand_draws(device, philox, draws: int = 2):
+    """Undo claim_rand_draws when the launch it was made for did not run: the generator's offset
+    goes back to the claimed one if nothing has drawn from it since."""
+    dev = torch.device(device)
+    gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+    if gen.initial_seed() == philox[0] and gen.get_offset() == philox[1] + 4 * draws:
+        gen.set_offset(philox[1])
 
 
 def sample_offsets(rand_q, rand_k, keep: int = 32):

@@ -359,7 +359,10 @@ class TDMTrainStep:
         if self.uncond is None:
             g = torch.Generator().manual_seed(1234)
             self.uncond = torch.randn(1, 1, x.shape[-1], generator=g) * 0.5
-        return self.uncond.to(device=x.device, dtype=x.dtype)
+        if self.uncond.device != x.device or self.uncond.dtype != x.dtype:
+            # moved once: a pageable host copy per teacher call would sync the timed step
+            self.uncond = self.uncond.to(device=x.device, dtype=x.dtype)
+        return self.uncond
 
     def teacher_predict(self, x_noisy, cond):
         """predictor.predict(transformer_real, ..., cfg=args.cfg) (:1712, :1475-1498): with cfg,
