@@ -352,7 +352,10 @@ def run(args):
                             pt["hbm_gbs_counters"] = round(gbs, 1)
                             pt["hbm_frac_counters"] = round(gbs / PEAK_HBM_GBS, 4)
                             pt["traffic_detail"] = tr
-            result["backward"] = measure_backward("cog", dev)
+            # the training path's backward of both TDM-trained variants (CogVideoX first: the
+            # headline's model; Wan's sibling TDM script trains the D=128 geometry)
+            result["backward"] = [measure_backward("cog", dev), measure_backward("wan", dev)]
+            result["end_to_end"] = measure_end_to_end(dev, ms_per_call, calls, frames)
         if world == 1 and not args.no_cpu_baseline:
             base = "cog" if args.variant == "cog-ml" else args.variant
             result["cpu_baseline"] = cpu_baseline_sdpa(base)
@@ -591,6 +594,97 @@ def measure_backward(variant, dev, reps=6):
             # the deterministic design (no atomics) recomputes S and dP in the dQ kernel: 7 GEMMs
             # of the forward's size per kept block pair are executed against the 5 counted above
             "executed_gemm_frac": round(tfs * 7 / 5 / PEAK_BF16_TFLOPS, 4)}
+
+
+class _StandInCogVideoXBlock(torch.nn.Module):
+    """One CogVideoX-5B transformer block's compute at its real dimensions with random weights
+    (diffusers' CogVideoXBlock: norm1 -> to_q/to_k/to_v -> per-head LayerNorm on q and k ->
+    inner_attention -> to_out, gated residual; norm2 -> FFN 3072 -> 12288 -> 3072, GELU(tanh), gated
+    residual). The adaLN modulation is a per-block constant here (its time-embedding MLP is
+    O(hidden^2) per step, not per token) and RoPE is omitted (elementwise on q/k). Stand-in for
+    timing only: no weights are available offline, so nothing about its outputs is claimed."""
+
+    def __init__(self, hidden, heads, ffn, inner_attention, dev, gen):
+        super().__init__()
+        kw = dict(device=dev, dtype=torch.bfloat16)
+
+        def w(o, i):
+            return (torch.randn(o, i, device=dev, generator=gen) * (i ** -0.5)).to(torch.bfloat16)
+        self.heads = heads
+        self.qkv = w(3 * hidden, hidden)
+        self.qkv_b = torch.zeros(3 * hidden, **kw)
+        self.out = w(hidden, hidden)
+        self.ff1, self.ff2 = w(ffn, hidden), w(hidden, ffn)
+        self.mod = (torch.randn(6, hidden, device=dev, generator=gen) * 0.1).to(torch.bfloat16)
+        self.inner_attention = inner_attention
+
+    def forward(self, x):
+        import torch.nn.functional as F
+        B, L, C = x.shape
+        sh1, sc1, g1, sh2, sc2, g2 = self.mod
+        h = F.layer_norm(x, (C,)) * (1 + sc1) + sh1
+        qkv = F.linear(h, self.qkv, self.qkv_b).view(B, L, 3, self.heads, C // self.heads)
+        q, k, v = (F.layer_norm(qkv[:, :, i], (C // self.heads,)).transpose(1, 2) if i < 2
+                   else qkv[:, :, i].transpose(1, 2) for i in range(3))
+        o = self.inner_attention(q, k, v).transpose(1, 2).reshape(B, L, C)
+        x = x + g1 * F.linear(o, self.out)
+        h = F.layer_norm(x, (C,)) * (1 + sc2) + sh2
+        return x + g2 * F.linear(F.gelu(F.linear(h, self.ff1), approximate="tanh"), self.ff2)
+
+
+def measure_end_to_end(dev, attn_ms_per_call, calls, frames, steps=8):
+    """SURVEY §8(d) end-to-end stand-in: one CogVideoX-5B 8-step video through 42 stand-in blocks at
+    the model's dimensions (hidden 3072 = 48 heads x 64, FFN 4x, 226 text + 17550 video tokens,
+    batch 1: guidance_scale 1 as at cogvideox/train/inference.py:85-90), bf16 GEMMs through
+    PyTorch-ROCm (hipBLASLt), the HIP sparse attention inside every block. The scheduler step and
+    the VAE are out of scope (parity unpinned: diffusers and the weights are absent)."""
+    import vblade
+    V = VARIANTS["cog"]
+    H, layers = V["H"], V["layers"]
+    hidden = H * V["D"]
+    attn = vblade.AdaptiveBlockSparseAttn("cog", log_every=0)
+    L = attn.gilbert_rearranger.seq_len
+    gen = torch.Generator(device=dev).manual_seed(77)
+    blocks = [_StandInCogVideoXBlock(hidden, H, 4 * hidden, attn, dev, gen) for _ in range(layers)]
+    x0 = torch.randn(1, L, hidden, device=dev, dtype=torch.bfloat16, generator=gen)
+
+    def video():
+        x = x0
+        for _ in range(steps):
+            for blk in blocks:
+                x = blk(x)
+        return x
+
+    def timed():
+        video()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        video()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    with torch.no_grad():
+        sec = timed()
+        # the same video with the attention replaced by `v` (no attention at all): the difference
+        # is the attention path's share inside the model (its inputs are the stand-in's q/k/v, so
+        # its mask density is the energy rule's on them, not the synthetic inputs' of the headline)
+        for blk in blocks:
+            blk.inner_attention = lambda q, k, v: v
+        sec_null = timed()
+    gemm_flops = 2.0 * L * (3 * hidden * hidden + hidden * hidden + 2 * hidden * 4 * hidden) * layers * steps
+    att_s = sec - sec_null
+    sparsity = attn.sparsity
+    del blocks, x0
+    torch.cuda.empty_cache()
+    return {"what": "CogVideoX-5B 8-step video, 42 stand-in blocks at the model's dimensions "
+                    "(random weights, batch 1, no VAE/scheduler), HIP sparse attention inside",
+            "frames_per_s": round(frames / sec, 3), "s_per_video": round(sec, 4),
+            "attention_s_per_video": round(att_s, 4),
+            "attention_fraction": round(att_s / sec, 4),
+            "attention_sparsity": round(sparsity, 4),
+            "headline_attention_s_per_video": round(attn_ms_per_call * 1e-3 * calls, 4),
+            "gemm_tflop_per_video": round(gemm_flops / 1e12, 1),
+            "non_attention_tflops": round(gemm_flops / sec_null / 1e12, 1)}
 
 
 def quality_vs_oracle(mod, qkv, variant):

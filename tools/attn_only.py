@@ -60,7 +60,7 @@ with torch.no_grad():
     kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
     # the module's K/V source (gather_kv="auto": gathered rows at D=128, Gilbert copies at D=64), so
     # the counters describe the same kernel variant that bench.py times
-    gather = (D == 128) if m.gather_kv == "auto" else bool(m.gather_kv)
+    gather = m._gather(D)
     k_src, v_src, kv_rows = (k, v, rows) if gather else (k_r, v_r, None)
     for _ in range(n):
         if what in ("attn", "all"):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: how often the forward's lazy-max slow path fires (needs variants/lib_<tag>.so built
-with -DVB_LAZY_COUNT=1). usage: python tools/lazy_count.py TAG"""
+with -DVB_LAZY_COUNT=1). usage: python tools/diag/lazy_count.py TAG"""
 import ctypes
 import math
 import os
@@ -8,7 +8,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))

@@ -8,7 +8,7 @@ import torch
 
 OPT = sys.argv[sys.argv.index('--opt') + 1] if '--opt' in sys.argv else 'overlap'
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)
 import vblade  # noqa: E402

@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """rocprofv3 target: the predictor alone (score only) and whole calls, on one library variant.
-usage: python tools/pred_prof.py TAG [variant]"""
+usage: python tools/diag/pred_prof.py TAG [variant]"""
 import os
 import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)

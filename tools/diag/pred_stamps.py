@@ -2,14 +2,14 @@
 """Per-phase s_memtime sums of the predictor's score kernel (diagnostic build: tools/build_variant.sh
 pstamp with VB_EXTRA_FLAGS=-DVB_PRED_STAMPS=1): per active wave, the cycles spent waiting for its
 K tile's DMA, at the barrier, issuing the next DMAs, in the whole loop body, and in the epilogue
-up to the Po row. usage: python tools/pred_stamps.py [cog|wan] [pred|call]"""
+up to the Po row. usage: python tools/diag/pred_stamps.py [cog|wan] [pred|call]"""
 import ctypes
 import os
 import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)

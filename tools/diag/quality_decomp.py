@@ -14,7 +14,7 @@ and for the energy rule plus fixed densities 0.3 / 0.5 / 0.7, compares on the GP
            kernel's pre-scaled Q and nothing else
 
 and prints one JSON line per case: max|.|, PSNR and bf16 ULP histograms of every pair.
-usage: python tools/quality_decomp.py [--variant cog|wan|both] [--out FILE]
+usage: python tools/diag/quality_decomp.py [--variant cog|wan|both] [--out FILE]
 """
 import argparse
 import json
@@ -25,7 +25,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import bsa_oracle as O  # noqa: E402

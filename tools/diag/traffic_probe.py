@@ -3,12 +3,12 @@
 for the Wan2.1 and CogVideoX points, on the predicted masks of the synthetic inputs and on a band
 mask with the same kept count per row (tools/attn_only.py "band"): whether the excess over the
 algorithmic bytes follows the kernel's traversal or the masks' locality.
-usage: python tools/traffic_probe.py [--out FILE]"""
+usage: python tools/diag/traffic_probe.py [--out FILE]"""
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 

@@ -161,9 +161,10 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self.overlap = bool(cfg.get("overlap", True))
         # The attention kernel gathers K/V rows through the Gilbert index (True) or streams the
         # Gilbert-ordered contiguous copies the pooled pass writes (False: 2·L·D·2 bytes more per
-        # head, written beside the predictor). "auto" (default) takes what measured faster per
-        # head dim (tools/overlap_ab.py --opt gather_kv): gather at D=128 (Wan, +2.4 % per call),
-        # copies at D=64 (CogVideoX, +0.9 %).
+        # head, written beside the predictor). "auto" (default): copies whenever the one-wave-per-SIMD
+        # forward runs (it takes only them); with VB_FWD1=0 what measured faster per head dim for
+        # attn_fwd_kernel (tools/diag/overlap_ab.py --opt gather_kv): gather at D=128 (Wan, +2.4 % per
+        # call), copies at D=64 (CogVideoX, +0.9 %).
         self.gather_kv = cfg.get("gather_kv", "auto")
 
     # -------------------------------------------------------------------------------- helpers
@@ -175,6 +176,12 @@ class AdaptiveBlockSparseAttn(nn.Module):
             r = r.to(device)
             self.gilbert_rearranger.rows = r
         return r
+
+    def _gather(self, D: int) -> bool:
+        if self.gather_kv != "auto":
+            return bool(self.gather_kv)
+        # the one-wave-per-SIMD forward (vb_attn_fwd1.hip) streams contiguous copies only
+        return D == 128 and not ops.FWD1
 
     def _count_slot(self, device):
         if self._kept_slots is None or self._kept_slots.device != device:
@@ -259,7 +266,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
             # predictor's score-kernel launch, beside the MFMA-bound score workgroups (overlap=True),
             # or after it (overlap=False)
             ride = fused and self.overlap
-            gather = (D == 128) if self.gather_kv == "auto" else bool(self.gather_kv)
+            gather = self._gather(D)
             copies = not (gather and rows is not None)
             outs = ops.pool_kv_outputs(k, self.sample_gap, reordered=copies) if ride else None
             with torch.no_grad():
@@ -273,7 +280,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
             mask = block_mask.to(torch.uint8)
             count.add_(mask.sum())
             if fused:
-                gather = (D == 128) if self.gather_kv == "auto" else bool(self.gather_kv)
+                gather = self._gather(D)
                 pooled = ops.pool_kv(k, v, self.sample_gap, rows, reordered=not (gather and rows is not None))
         self._slot_totals.append(B * H * nb * nb)
         self.sparsity_counter += 1

@@ -411,6 +411,9 @@ def _mask_predict(q, k, q_off, k_off, *, rows, energy_threshold, min_keep, max_k
 # generator's Philox offset by 4.
 RAND_ONE_PASS_NUMEL = 524288   # the MI355X value; rand_one_pass_numel(device) is the per-device bound
 PHILOX_DRAWS = os.environ.get("VB_PHILOX_DRAWS", "1") != "0"   # off: the callers use torch.rand
+# VB_FWD1=1 selects the one-wave-per-SIMD inference forward (vb_attn_fwd1.hip) in the library and
+# the K/V source it needs here (the library reads the same variable; default: attn_fwd_kernel)
+FWD1 = os.environ.get("VB_FWD1", "0") != "0"
 _ONE_PASS = {}
 
 
