@@ -136,6 +136,36 @@ def realistic_qkv(H, L, D, seed, device):
     return q, k, v
 
 
+# latent token grids (width, height, frames) and text tokens of the two workloads (caller order:
+# text first, then the video tokens frame-major, row-major: cogvideo_blocksparseattn.py:141-154)
+LATENT_GRID = {"cog": (45, 30, 13, 226), "cog-ml": (45, 30, 13, 226), "wan": (52, 30, 21, 0)}
+
+
+def local_qkv(variant, H, D, seed, device, waves=8, amp=2.0):
+    """Locality-faithful synthetic inputs: q, k = N(0,1) + amp * c(x, y, t) with
+    the centre c a smooth function of the token's latent coordinate — a sum of `waves` random
+    low-frequency plane waves (0-2 periods across each axis) with random D-vectors per head — so
+    tokens near each other in the video, and therefore the Gilbert-ordered 128-token blocks, share
+    centres as real video attention does. Text tokens get independent random centres."""
+    W, Hh, T, text = LATENT_GRID[variant]
+    g = torch.Generator(device=device).manual_seed(seed)
+    t, y, x = torch.meshgrid(torch.arange(T, device=device), torch.arange(Hh, device=device),
+                             torch.arange(W, device=device), indexing="ij")
+    pos = torch.stack([x.flatten() / W, y.flatten() / Hh, t.flatten() / T], 1).float()   # [Lv, 3]
+    freq = torch.randint(0, 3, (waves, 3), generator=g, device=device).float()
+    phase = torch.rand(waves, generator=g, device=device) * 2 * math.pi
+    basis = torch.cos(2 * math.pi * pos @ freq.T + phase)                               # [Lv, waves]
+    a = torch.randn(1, H, waves, D, generator=g, device=device) / math.sqrt(waves / 2)
+    cent = basis @ a                                                                    # [1, H, Lv, D]
+    if text:
+        cent = torch.cat([torch.randn(1, H, text, D, generator=g, device=device), cent], 2)
+    L = cent.shape[2]
+    q = (torch.randn(1, H, L, D, generator=g, device=device) + amp * cent).bfloat16()
+    k = (torch.randn(1, H, L, D, generator=g, device=device) + amp * cent).bfloat16()
+    v = torch.randn(1, H, L, D, generator=g, device=device).bfloat16()
+    return q, k, v
+
+
 def ml_attn_flops(mask: torch.Tensor, L: int, D: int) -> float:
     """Algorithmic FLOPs of one multi-level launch: sum over (i,j) with level p in {1,2,4,8} of
     4*m_i*(128/p)*D (m_i the true query-block size; key blocks are full pyramid blocks, as the
@@ -338,13 +368,18 @@ def run(args):
             result["points"] = [measure_point(v, d, dev, dense_cache)
                                 for v, d in (("wan", None), ("cog-ml", None), ("cog", 0.05),
                                              ("cog", 0.3), ("cog", 0.5), ("cog", 0.7))]
+            # the energy rule on locality-faithful inputs (neighbouring Gilbert blocks share
+            # centres, as video does): mask density and counter traffic of both workloads
+            result["points"] += [measure_point(v, None, dev, dense_cache, inputs="local")
+                                 for v in ("cog", "wan")]
             if not args.no_pmc:
                 # counter-measured HBM-side traffic of the attention kernel at the Wan point and at
                 # the high-sparsity point (density 0.05), as GB/s against the 8 TB/s peak
                 for pt in result["points"]:
-                    if (pt["variant"], pt["mask"]) in (("wan", "energy rule"), ("cog", "density 0.05")):
+                    local = pt["inputs"].startswith("locality")
+                    if (pt["variant"], pt["mask"]) in (("wan", "energy rule"), ("cog", "density 0.05")) or local:
                         d = None if pt["mask"] == "energy rule" else 0.05
-                        tr = pmc_traffic(pt["variant"], density=d)
+                        tr = pmc_traffic(pt["variant"], density=d, local=local)
                         if tr is not None:
                             gbs = tr["bytes"] / (pt["attn_fwd_ms"] * 1e-3) / 1e9
                             pt["traffic"] = tr["bytes"]
@@ -466,7 +501,7 @@ def measure_kernels(mod, sets, L, H, D, dev, args, events, rng_state, calls):
     return out
 
 
-def measure_point(variant, density, dev, dense_cache, calls=None, seed=500, every=4):
+def measure_point(variant, density, dev, dense_cache, calls=None, seed=500, every=4, inputs="blocks"):
     """One more operating point, measured in-process on fresh resident inputs: one denoising
     step's calls (layers) of the whole module, timed with events, the attention launches timed
     individually, and their FLOPs replayed from the same RNG state (as the main line)."""
@@ -483,7 +518,8 @@ def measure_point(variant, density, dev, dense_cache, calls=None, seed=500, ever
         mod = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **over)
     L = mod.gilbert_rearranger.seq_len
     Lkp = 0 if ml else (L + mod.sample_gap - 1) // mod.sample_gap
-    sets = [realistic_qkv(H, L, D, seed + s, dev) for s in range(2)]
+    sets = [realistic_qkv(H, L, D, seed + s, dev) if inputs == "blocks" else local_qkv(variant, H, D, seed + s, dev)
+            for s in range(2)]
     with torch.no_grad():
         for c in range(4):
             mod(*sets[c % 2])
@@ -528,8 +564,11 @@ def measure_point(variant, density, dev, dense_cache, calls=None, seed=500, ever
     sparsity = mod.sparsity_acc / mod.sparsity_counter if ml else mod.sparsity
     res = {
         "variant": variant,
+        "inputs": ("block-structured (centres per caller-order 128-token run)" if inputs == "blocks"
+                   else "locality-faithful (centres a smooth function of the latent x,y,t)"),
         "mask": ("rank-band level mask (reference mask_ratios)" if ml
                  else "energy rule" if density is None else f"density {density}"),
+        "mask_density": round(float(mod.last_mask.float().mean().item()), 4) if not ml else None,
         "mean_sparsity": round(sparsity, 4),
         "frames_per_s": round(frames / (ms_call * 1e-3 * DENOISE_STEPS * layers), 3),
         "ms_per_call": round(ms_call, 4),
@@ -695,6 +734,7 @@ def quality_vs_oracle(mod, qkv, variant):
     distance from (b)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import bsa_oracle as O
+    from vblade import ops
     q, k, v = qkv
     out = mod(q, k, v)
     mask = mod.last_mask[:, :1].bool().cpu()
@@ -712,6 +752,9 @@ def quality_vs_oracle(mod, qkv, variant):
 
     h_ref, h_ex, h_re = (O.bf16_ulp_histogram(a, b) for a, b in ((got, ref), (got, exact), (ref, exact)))
     return {"head": 0, "psnr_db": psnr(got, ref),
+            # how head_mask_type = ones(H) reads the predicted masks
+            "mask_head_mode": mod.mask_head_mode,
+            "forward_kernel": "attn_fwd1_kernel (one wave per SIMD)" if ops.FWD1 else "attn_fwd_kernel",
             "max_abs": round((got - ref).abs().max().item(), 5),
             "ulp_hist": h_ref["ulp_hist"], "max_ulp": h_ref["max_ulp"],
             "vs": "oracle/bsa_oracle.adaptive_attention (reference rounding), same mask",
@@ -723,7 +766,7 @@ def quality_vs_oracle(mod, qkv, variant):
                                    "ulp_hist": h_re["ulp_hist"], "max_ulp": h_re["max_ulp"]}}
 
 
-def pmc_traffic(variant, timeout=300, density=None, band=False):
+def pmc_traffic(variant, timeout=300, density=None, band=False, local=False):
     """HBM-side bytes per attn_fwd_kernel launch from rocprofv3 PMC counters, one counter per
     pass (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
     tallies wide coalesced reads at half their bytes, so traffic = 2*FETCH + WRITE. The target
@@ -737,7 +780,7 @@ def pmc_traffic(variant, timeout=300, density=None, band=False):
         d = tempfile.mkdtemp(prefix="vb_pmc_", dir="/tmp")
         cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.join(ROOT, "tools", "attn_only.py"), variant, "3", "attn",
-               "none" if density is None else str(density)] + (["band"] if band else [])
+               "none" if density is None else str(density)] + (["band"] if band else ["local"] if local else [])
         try:
             subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, check=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
@@ -747,7 +790,8 @@ def pmc_traffic(variant, timeout=300, density=None, band=False):
         xs = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if "attn_fwd_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                kn = r.get("Kernel_Name", "")
+                if ("attn_fwd_kernel" in kn or "attn_fwd1_kernel" in kn) and r.get("Counter_Name") == counter:
                     xs.append(float(r["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not xs:

@@ -5,7 +5,9 @@ usage: attn_only.py [cog|wan|cog-ml] [N] [attn|pred|all] [density (fixed kept fr
 the energy rule)] [band]
 "band": the predicted mask replaced by a diagonal band with the same kept count per row (plus the
 forced tail rows/columns) — a mask whose neighbouring q-blocks share key blocks, as the synthetic
-random-centre inputs' masks do not (the L2-locality control for the traffic counters)."""
+random-centre inputs' masks do not (the L2-locality control for the traffic counters).
+"local": the locality-faithful inputs (bench.local_qkv: centres a smooth function of the latent
+x, y, t) and the energy rule's mask on them."""
 import os
 import sys
 
@@ -16,7 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)
 import vblade  # noqa: E402
 from vblade import ops  # noqa: E402
-from bench import realistic_qkv  # noqa: E402
+from bench import local_qkv, realistic_qkv  # noqa: E402
 
 variant = sys.argv[1] if len(sys.argv) > 1 else "cog"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
@@ -42,8 +44,9 @@ over = {} if density is None else dict(min_retain_ratio=density, max_retain_rati
 m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0, **over)
 L = m.gilbert_rearranger.seq_len
 dev = torch.device("cuda")
+local = len(sys.argv) > 5 and sys.argv[5] == "local"
 with torch.no_grad():
-    q, k, v = realistic_qkv(H, L, D, 0, dev)
+    q, k, v = local_qkv(variant, H, D, 0, dev) if local else realistic_qkv(H, L, D, 0, dev)
     rows = m._rows(dev)
     qo = vblade.draw_sample_offsets(1, H, dev)
     ko = vblade.draw_sample_offsets(1, H, dev)

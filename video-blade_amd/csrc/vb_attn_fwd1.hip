@@ -36,9 +36,13 @@ namespace vb {
 #define VB_FWD1_OCC64 1   // workgroups per CU the D=64 kernel is register-budgeted for
 #endif
 #ifndef VB_FWD1_SCHED
-#define VB_FWD1_SCHED 1   // sched_group_barrier interleave of the two regions (0: the compiler's order)
+#define VB_FWD1_SCHED 2   // 2: every filler placed by hand (sched_barrier per MFMA gap); 1: sched_group_barrier
+                          // interleave of the two regions; 0: the compiler's order
 #endif
 
+#ifndef VB_FWD1_NODMA
+#define VB_FWD1_NODMA 0   // diagnostic builds only: no LDS-DMA after the prologue (stale tiles, wrong results)
+#endif
 #ifndef VB_FWD1_RING64
 #define VB_FWD1_RING64 6   // K and V ring slots at D=64 (one workgroup per CU; 4 at two)
 #endif
@@ -541,9 +545,196 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 #pragma unroll
     for (int r = 0; r < 16; ++r) cb[r] += p.pool_bias_l2;
   }
+  // ---- the same iteration with every instruction group placed by hand ---------------------------
+  // Each MFMA gets a fixed set of fillers, pinned by sched_barrier: the exps of S(t) spread evenly
+  // (16 per region), each exp's row-sum add and the bf16 pack of each finished pair one gap later
+  // (off the exp's latency), the LDS reads of the operands two or more gaps before their MFMA, and
+  // the LDS-DMA pieces in the gaps after the region's reads (the DMA writes LDS; it goes last).
+  auto body_placed = [&](int t, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+    constexpr int cur = u & 1, nxt = cur ^ 1;
+    constexpr int kSlotK1 = ((u + 1) % kRing) * kMatBytes;
+    constexpr int kSlotV = (u % kRing) * kMatBytes;
+    constexpr int nA = 2 * DT + KS;      // MFMAs per region (the same count in both)
+    constexpr int epg = 16 / nA;         // exps per gap: 2 at D=64, 1 at D=128
+    F1_STAMP(b0);
+    VB_WAIT_VMCNT((kRing - 2) * kPieces);
+    lgkm_wait(vlo23, vhi23);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    F1_STAMP(b1);
+    F1_ACC(0, b1 - b0);
+    // this iteration's DMA descriptor (scalar work, before the MFMA stream)
+    const int tt = t + kRing - my_mat;
+    const int slot_off = my_mat == 0 ? (u % kRing) * kMatBytes : kVBase + ((u + kRing - 1) % kRing) * kMatBytes;
+    const int blk = __builtin_amdgcn_readfirstlane(blk_dma);
+    const bool pooled = tt >= ntm;
+    int kstart = blk * kQBlk + (tt & 1) * kKT;
+    const uint8_t* dbase = my_mbase;
+    int dbytes = main_bytes;
+    if (pooled) {
+      kstart = (tt - ntm) * kKT;
+      dbase = my_pbase;
+      dbytes = pool_bytes;
+    }
+    const int soff = kstart * my_rowb;
+    dbytes = tt >= ntiles ? 0 : dbytes - soff;
+    const srd_t sd{dbase + soff, dbytes};
+    uint8_t* dma_dst = smem + slot_off + sub * kPieces * 1024;
+    __builtin_amdgcn_sched_barrier(0);
+
+    V8 kf0[KS], kf1[KS];
+    float e[16], h4[4];
+    u32x4 pk[2];
+    // fillers of gap g for the 16 exps of x: exps of gap g, adds + packs of gap g-1
+    auto fill = [&](const f32x16& x, int g) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < epg; ++j) {
+        const int r = g * epg + j;
+        if (r < 16) e[r] = exp2_fast(x[r]);
+      }
+#pragma unroll
+      for (int j = 0; j < epg; ++j) {
+        const int r = (g - 1) * epg + j;
+        if (r >= 0 && r < 16) {
+          if (r < 4) h4[r] = e[r];
+          else h4[r & 3] += e[r];
+          if (r & 1) {
+            // the pack stays in this gap: hipcc would otherwise sink it past the overflow
+            // check (the check's slow path recomputes the packs)
+            pk[r >> 3][(r & 7) >> 1] = pack2<T>(e[r - 1], e[r]);
+            asm volatile("" : "+v"(pk[r >> 3][(r & 7) >> 1]));
+          }
+        }
+      }
+    };
+    // the tail of the filler stream after the last gap: adds and packs of the last gap's exps
+    auto finish = [&](V8& p0, V8& p1) __attribute__((always_inline)) -> float {
+#pragma unroll
+      for (int j = 0; j < epg; ++j) {
+        const int r = (nA - 1) * epg + j;
+        if (r >= 4 && r < 16) h4[r & 3] += e[r];
+        if (r < 16 && (r & 1)) {
+          pk[r >> 3][(r & 7) >> 1] = pack2<T>(e[r - 1], e[r]);
+          asm volatile("" : "+v"(pk[r >> 3][(r & 7) >> 1]));
+        }
+      }
+#pragma unroll
+      for (int r = nA * epg; r < 16; ++r) {   // exps that did not fit the gaps (none at 16 / nA)
+        e[r] = exp2_fast(s[cur][0][r]);
+      }
+      p0 = __builtin_bit_cast(V8, pk[0]);
+      p1 = __builtin_bit_cast(V8, pk[1]);
+      return (h4[0] + h4[1]) + (h4[2] + h4[3]);
+    };
+
+    // ======== region A: P(t-1).V(t-1) k-steps 2,3 | S(t+1) keys 0..31 ; exps of S(t) keys 0..31 ====
+#pragma unroll
+    for (int g = 0; g < nA; ++g) {
+      if (g < 2 * DT) {
+        const int kk = g / DT, dt = g % DT;
+        o[dt] = T::mfma32(join8<T>(vlo23[kk][dt], vhi23[kk][dt]), pp[kk], o[dt]);
+      } else {
+        const int ks = g - 2 * DT;
+        s[nxt][0] = T::mfma32(kf0[ks], qf[ks], ks == 0 ? cb : s[nxt][0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // the MFMA opens its gap
+      fill(s[cur][0], g);
+      // LDS reads, two per gap: K(t+1) keys 0..31, K(t+1) keys 32..63, then V(t) k-steps 0, 1
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int d = 2 * g + j;
+        if (d < KS) kf0[d] = lds_b128<T>(smem + kSlotK1, k_lane[d]);
+        else if (d < 2 * KS) kf1[d - KS] = lds_b128<T>(smem + kSlotK1 + 32 * kRowB, k_lane[d - KS]);
+        else if (d < 2 * KS + 4 * DT) {
+          const int v = d - 2 * KS;               // kk = v / (2 DT), dt = (v / 2) % DT, lo/hi = v & 1
+          const int kk = v / (2 * DT), dt = (v / 2) % DT;
+          const int r0 = (kk >> 1) * 32 + 16 * (kk & 1) + 8 * (v & 1);
+          s16x4 x = lds_tr4_asm(v_lane[dt], kSlotV + r0 * kRowB);
+          if (v & 1) vhi01[kk][dt] = x;
+          else vlo01[kk][dt] = x;
+        }
+      }
+      // LDS-DMA pieces, one per gap, in the gaps after the reads
+      {
+        const int i = g - (nA - kPieces);
+        if (i >= 0 && i < kPieces && !VB_FWD1_NODMA) dma16(sd, dma_dst + i * 1024, vo[i], 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    float hs0 = finish(pf01[0], pf01[1]);
+    if (!__all(hs0 <= kLazyBound)) {
+      asm volatile("");
+      raise_m(half_max(s[cur][0]), s[cur][0], s[cur][1], s[nxt][0]);
+      hs0 = exp_pack(s[cur][0], pf01[0], pf01[1]);
+    }
+    l += hs0;
+    F1_STAMP(b2);
+    F1_ACC(1, b2 - b1);
+
+    // ======== region B: S(t+1) keys 32..63 | P(t).V(t) k-steps 0,1 ; exps of S(t) keys 32..63 ====
+    int blk_s2 = 0, blk_dma_next = 0;
+#pragma unroll
+    for (int g = 0; g < nA; ++g) {
+      if (g < KS) {
+        s[nxt][1] = T::mfma32(kf1[g], qf[g], g == 0 ? cb : s[nxt][1]);
+      } else {
+        if (g == KS) lgkm_wait(vlo01, vhi01);   // region A's V reads (no region-B read is older)
+        const int kk = (g - KS) / DT, dt = (g - KS) % DT;
+        o[dt] = T::mfma32(join8<T>(vlo01[kk][dt], vhi01[kk][dt]), pf01[kk], o[dt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      fill(s[cur][1], g);
+      if (g == 0) blk_s2 = blk_of(t + 2);
+      if (g == 1) blk_dma_next = blk_of(t + kRing + 1 - my_mat);
+      // V(t) k-steps 2, 3 for the next iteration, after the P.V MFMAs started (two per gap)
+      if (g >= KS) {
+#pragma unroll
+        for (int j = 0; j < 4 * DT / (nA - KS); ++j) {
+          const int v = (g - KS) * (4 * DT / (nA - KS)) + j;
+          const int kk = v / (2 * DT), dt = (v / 2) % DT;
+          const int r0 = ((kk + 2) >> 1) * 32 + 16 * ((kk + 2) & 1) + 8 * (v & 1);
+          s16x4 x = lds_tr4_asm(v_lane[dt], kSlotV + r0 * kRowB);
+          if (v & 1) vhi23[kk][dt] = x;
+          else vlo23[kk][dt] = x;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    float hs1 = finish(pp[0], pp[1]);
+    if (!__all(hs1 <= kLazyBound)) {
+      asm volatile("");
+      raise_m(half_max(s[cur][1]), s[cur][1], s[nxt][0], s[nxt][1]);
+      hs1 = exp_pack(s[cur][1], pp[0], pp[1]);
+    }
+    l += hs1;
+    F1_STAMP(b3);
+    F1_ACC(2, b3 - b2);
+    const int kl1 = klen_of(t + 1, blk_s1);
+    if (kl1 < kKT) {
+      asm volatile("");
+      mask_tail(s[nxt][0], 0, kl1);
+      mask_tail(s[nxt][1], 1, kl1);
+    }
+    if constexpr (kPool) {
+      if (t + 2 == ntm) {
+        asm volatile("");
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cb[r] += p.pool_bias_l2;
+      }
+    }
+    blk_s1 = blk_s2;
+    blk_dma = blk_dma_next;
+    F1_STAMP(b4);
+    F1_ACC(3, b4 - b3);
+  };
+
   // the body instantiated once per (ring slot, S parity) phase: every LDS offset an immediate
   auto run_phase = [&](int t0, auto U) __attribute__((always_inline)) {
-    if (t0 + decltype(U)::value < ntiles) body(t0 + decltype(U)::value, U);
+    if (t0 + decltype(U)::value < ntiles) {
+      if constexpr (VB_FWD1_SCHED == 2) body_placed(t0 + decltype(U)::value, U);
+      else body(t0 + decltype(U)::value, U);
+    }
   };
   for (int t0 = 0; t0 < ntiles; t0 += kPeriod)
     for_phases([&](auto U) __attribute__((always_inline)) { run_phase(t0, U); },
