@@ -1,11 +1,11 @@
-// Block-sparse FMHA forward, inference form, one wave per SIMD (gfx950 / MI355X).
+// Block-sparse FMHA forward, inference form, one compute wave per SIMD (gfx950 / MI355X).
 //
 // Same semantics as attn_fwd_kernel's lazy (inference) launches (vb_attn_fwd.hip: the reference's
 // block_sparse_attn_func forward as called at cogvideo_blocksparseattn.py:316-320 fused with the
 // pooled-KV branch and LSE combine of :367-393), built on a different machine model:
 //
-//  * a workgroup = 4 waves = one 128-row q-block (32 rows per wave), ONE workgroup per CU, so each
-//    wave is alone on its SIMD. The D=64 loop is bound by the SIMD's vector-issue port (two
+//  * a workgroup = one 128-row q-block, 4 compute waves of 32 rows, ONE workgroup per CU, so each
+//    compute wave is alone on its SIMD. The D=64 loop is bound by the SIMD's vector-issue port (two
 //    v_exp_f32, two adds and one bf16 pack per MFMA), and MFMA and VALU work of two waves sharing
 //    a SIMD barely overlap (profiles/r02_mfma_valu_overlap.json: 0.955 of the sum); inside ONE wave
 //    the VALU issues in the shadow of the wave's own MFMAs (0.71 of the sum, and a gap holds
@@ -16,11 +16,12 @@
 //                  beside exp2/sum/pack of S(t)[keys 0..31]
 //        region B: S(t+1)[keys 32..63]             and  P(t)[keys 0..31] . V(t)
 //                  beside exp2/sum/pack of S(t)[keys 32..63]
-//    The instruction interleave inside a region is fixed with sched_group_barrier.
-//  * K and V stream through separate 3-slot LDS rings by LDS-DMA, K two tiles and V one tile
-//    ahead of their first use (K(t+3) and V(t+2) are issued in iteration t), one barrier per tile.
-//    Issues past the last tile use a zero-extent buffer descriptor (no memory access), so every
-//    vmcnt is a constant.
+//    Every MFMA opens a gap whose fillers are placed by hand (sched_barrier around each gap).
+//  * K and V stream through separate R-slot LDS rings by LDS-DMA with R-1 tiles of lead (K(t+R)
+//    and V(t+R-1) are issued in iteration t), one barrier per tile. Issues past the last tile use a
+//    zero-extent buffer descriptor (no memory access), so every vmcnt is a constant. With kProd the
+//    DMA is issued by 4 producer waves (one beside each compute wave; a VMEM-only wave takes no
+//    VALU issue slots from its SIMD partner), otherwise by the compute waves in their gaps.
 //
 // The lazy running max, the overflow check per half-tile and the exp2-domain seeding of the S
 // accumulator are attn_fwd_kernel's (see there). A failing check rescales everything still at
@@ -35,13 +36,15 @@ namespace vb {
 #ifndef VB_FWD1_OCC64
 #define VB_FWD1_OCC64 1   // workgroups per CU the D=64 kernel is register-budgeted for
 #endif
-#ifndef VB_FWD1_SCHED
-#define VB_FWD1_SCHED 2   // 2: every filler placed by hand (sched_barrier per MFMA gap); 1: sched_group_barrier
-                          // interleave of the two regions; 0: the compiler's order
+#ifndef VB_FWD1_PROD64
+#define VB_FWD1_PROD64 0  // D=64: 4 producer waves issue the LDS-DMA (8-wave workgroups)
 #endif
-
 #ifndef VB_FWD1_NODMA
 #define VB_FWD1_NODMA 0   // diagnostic builds only: no LDS-DMA after the prologue (stale tiles, wrong results)
+#endif
+#ifndef VB_FWD1_ABL
+#define VB_FWD1_ABL 0     // diagnostic ablations (wrong results): bit 0 no LDS reads in the loop, bit 1 no
+                          // v_exp (the adds/packs stay), bit 2 no filler VALU at all
 #endif
 #ifndef VB_FWD1_RING64
 #define VB_FWD1_RING64 6   // K and V ring slots at D=64 (one workgroup per CU; 4 at two)
@@ -54,8 +57,8 @@ namespace vb {
 #define VB_DIAG 0
 #endif
 #if VB_DIAG
-// diagnostic builds only: per-segment s_memtime sums over all waves ([0] wait+barrier, [1] region
-// A, [2] region B, [3] end of iteration, [4] prologue, [5] epilogue, [8] tiles)
+// diagnostic builds only: per-segment s_memtime sums over the compute waves ([0] wait+barrier, [1]
+// region A, [2] region B, [3] end of iteration, [4] prologue, [5] epilogue, [8] tiles, [9] WGs)
 __device__ unsigned long long g_fwd1_stamp[16];
 __device__ __forceinline__ unsigned long long fwd1_stamp() {
   unsigned long long t;
@@ -83,17 +86,60 @@ __device__ __forceinline__ void lgkm_wait(s16x4 (&lo)[2][N], s16x4 (&hi)[2][N]) 
 #pragma unroll
     for (int d = 0; d < N; ++d) asm volatile("" : "+v"(lo[i][d]), "+v"(hi[i][d]));
 }
+// MFMAs with operands pinned to register files (D=128: O accumulates in AGPRs and Q is read from
+// AGPRs, so the ~330 live registers split over the two files without copies). hipcc's hazard
+// recognizer cannot see into these statements: a VALU that reads their results (or writes their
+// inputs) right after them needs the s_nop padding of hazard_pad() (only the rare paths do).
+// (The AGPR constraints exist only for the device pass: on the host pass "a" names x86's eax,
+// which these operands cannot bind, and clang then silently drops the kernels' host stubs.)
+template <class T>
+__device__ __forceinline__ void mfma_acc_a(f32x16& acc, const typename T::vec8& a, const typename T::vec8& b) {
+#if __HIP_DEVICE_COMPILE__
+  // s_nop 1: the two wait states a VALU write of a or b (join8's moves) needs before the MFMA
+  if constexpr (std::is_same<T, BF16>::value)
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+#endif
+}
+// d = a . b(AGPR) + c, all VGPR tuples except b
+template <class T>
+__device__ __forceinline__ f32x16 mfma_bq(const typename T::vec8& a, const typename T::vec8& b, const f32x16& c) {
+  f32x16 d = c;
+#if __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same<T, BF16>::value)
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(d) : "v"(a), "a"(b), "v"(c));
+  else
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %3" : "=&v"(d) : "v"(a), "a"(b), "v"(c));
+#endif
+  return d;
+}
+template <class T>
+__device__ __forceinline__ void mfma_bq_acc(f32x16& d, const typename T::vec8& a, const typename T::vec8& b) {
+#if __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same<T, BF16>::value)
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+  else
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+#endif
+}
+// Wait states between an asm MFMA and a VALU touching its registers (16-pass XDL). The registers
+// involved are operands of the padding statement, so no access to them can move across it.
+__device__ __forceinline__ void hazard_pad(f32x16 (&o)[4], f32x16& x, f32x16& y, f32x16& z) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4"
+               : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]), "+v"(x), "+v"(y), "+v"(z)::"memory");
+#endif
+}
 // f(integral_constant<int, U>) for U = 0 .. N-1, in order
 template <class F, int... Us>
 __device__ __forceinline__ void for_phases(F&& f, std::integer_sequence<int, Us...>) {
   (f(std::integral_constant<int, Us>{}), ...);
 }
-// sched_group_barrier masks
-constexpr int kMaskMFMA = 0x008, kMaskVALU = 0x002, kMaskDSR = 0x100, kMaskVMEM = 0x020;
 }  // namespace fwd1
 
-template <int D, class T, bool kPool, int kOcc>
-__global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdParams p) {
+template <int D, class T, bool kPool, int kOcc, bool kProd>
+__global__ void __launch_bounds__(kProd ? 2 * kThreads : kThreads, kOcc) attn_fwd1_kernel(const FwdParams p) {
   using namespace fwd1;
   using V8 = typename T::vec8;
   constexpr int KS = D / 16;                   // k-steps of S = K.Q^T
@@ -101,20 +147,24 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
   constexpr float kLazyBound = std::is_same<T, BF16>::value ? kLazyBoundBF16 : kLazyBoundF16;
   constexpr int kRowB = D * 2;
   constexpr int kMatBytes = kKT * kRowB;       // one 64-key K (or V) tile
-  // slots per ring: K(t+1) .. K(t+R-1) and V(t) .. V(t+R-2) are in flight or landed during tile t,
-  // i.e. R-1 tiles of lead for both (the LDS of one workgroup per CU allows it)
+  // slots per ring: K(t+1) .. K(t+R-1) and V(t) .. V(t+R-2) are in flight or landed during tile t
   constexpr int kRing = D == 64 ? (kOcc == 1 ? VB_FWD1_RING64 : 4) : VB_FWD1_RING128;
   constexpr int kPeriod = kRing % 2 ? 2 * kRing : kRing;   // slot phase x S-buffer parity
   constexpr int kVBase = kRing * kMatBytes;    // V ring after the K ring
   constexpr int kChunks = kRowB / 16;
   constexpr int kRowsPerInst = 1024 / kRowB;
-  constexpr int kPieces = kMatBytes / 1024 / 2;   // LDS-DMA pieces per wave and tile (2 waves per matrix)
+  constexpr int kPieces = kMatBytes / 1024 / 2;   // LDS-DMA pieces per DMA wave and tile (2 per matrix)
+  constexpr int nA = 2 * DT + KS;                 // MFMAs per region (both regions)
+  constexpr bool kRegSplit = D == 128;            // O in AGPRs, Q read from AGPRs (asm MFMAs)
+  constexpr int epg = 16 / nA;                    // exps per gap: 2 at D=64, 1 at D=128
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kRing * kMatBytes + kMaxBlocks * 2 + 16];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + 2 * kRing * kMatBytes);
   int* list_n = reinterpret_cast<int*>(smem + 2 * kRing * kMatBytes + kMaxBlocks * 2);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool producer = kProd && wave >= 4;   // wave-uniform
+  const int cw = wave & 3;                    // compute rows / DMA role of this wave
   const int half = lane >> 5;
   const int l32 = lane & 31;
 
@@ -138,20 +188,16 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
   if (q0 >= Lq) return;
   const int nbk = (Lk + kQBlk - 1) / kQBlk;
 
-  // ---- kept key blocks (diagonal first; see attn_fwd_kernel) --------------------------------------
-  const uint8_t* mrow = nullptr;
-  bool dense = true;
-  if (p.use_main && p.mask) {
-    dense = false;
-    mrow = p.mask + b * p.ms[0] + (int64_t)h * p.ms[1] + (int64_t)qblk * p.ms[2];
-  }
-  if (threadIdx.x < 64) {
+  // ---- kept key blocks (diagonal first; see attn_fwd_kernel); a producer wave builds the list ----
+  if (wave == (kProd ? 4 : 0)) {
+    const uint8_t* mrow = (p.use_main && p.mask) ? p.mask + b * p.ms[0] + (int64_t)h * p.ms[1] + (int64_t)qblk * p.ms[2]
+                                                 : nullptr;
     int n = 0;
     int dpos = -1;
     if (p.use_main) {
       for (int j0 = 0; j0 < nbk; j0 += 64) {
         const int j = j0 + lane;
-        const bool keep = (j < nbk) && (dense || mrow[j] != 0);
+        const bool keep = (j < nbk) && (mrow == nullptr || mrow[j] != 0);
         const unsigned long long bal = __ballot(keep);
         if (keep) {
           const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
@@ -175,12 +221,12 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
   }
 
   // ---- Q fragment, pre-scaled by scale*log2(e) (B operand of S^T = K.Q^T) -------------------------
-  const int qg = q0 + wave * 32 + l32;
+  const int qg = q0 + cw * 32 + l32;
   const bool qvalid = qg < Lq;
   int qrow = qvalid ? qg : Lq - 1;
-  if (p.q_rows) qrow = p.q_rows[qrow];
   V8 qf[KS];
-  {
+  if (!producer) {
+    if (p.q_rows) qrow = p.q_rows[qrow];
     const uint8_t* qp = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1]) +
                         (int64_t)qrow * 2 * p.qs[2];
 #pragma unroll
@@ -189,8 +235,16 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int e = 0; e < 8; ++e) qf[s][e] = T::from_f32(T::to_f32(qf[s][e]) * p.c);
+    // Q's home: AGPRs at D=128 (read there by the asm MFMAs), VGPRs otherwise
+    if constexpr (D == 128) {
+#if __HIP_DEVICE_COMPILE__
 #pragma unroll
-    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]));
+      for (int s = 0; s < KS; ++s) asm volatile("" : "+a"(qf[s]));
+#endif
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]));
+    }
   }
   __syncthreads();
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
@@ -199,9 +253,13 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
   const int ntp = kPool ? (p.Lkp + kKT - 1) / kKT : 0;
   const int ntiles = ntm + ntp;
 
-  // ---- LDS-DMA sources: waves 0-1 fill K tiles, waves 2-3 V tiles (kPieces 1-KiB pieces each) ----
-  const int my_mat = wave >> 1;
-  const int sub = wave & 1;
+  auto blk_of = [&](int tt) __attribute__((always_inline)) -> int {
+    return (int)list[min(max(tt, 0) >> 1, kMaxBlocks - 1)];
+  };
+
+  // ---- LDS-DMA sources: DMA roles 0-1 fill K tiles, 2-3 V tiles (kPieces 1-KiB pieces each) ------
+  const int my_mat = cw >> 1;
+  const int sub = cw & 1;
   const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1]);
   const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1]);
   // Row strides: main and pooled keys share one (the host launches this kernel only then), so a
@@ -217,8 +275,8 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
     my_pbase = my_mat == 0 ? kpb : vpb;
     pool_bytes = (int)((int64_t)(p.Lkp - 1) * my_rowb + kRowB);
   }
-  // lane's row of its first piece and the byte offset of every piece's 16-byte chunk within a tile
-  // (the K/V images' XOR swizzles applied on the source side, as attn_fwd_kernel does)
+  // the byte offset of every piece's 16-byte chunk within a tile (the K/V images' XOR swizzles
+  // applied on the source side, as attn_fwd_kernel does)
   const int row0 = sub * kPieces * kRowsPerInst + lane / kChunks;
   int vo[kPieces];
 #pragma unroll
@@ -234,40 +292,78 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
     }
     vo[i] = r * my_rowb + 16 * ch;
   }
-  const uint32_t smem_u32 = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)smem));
-  // Tile tt of this wave's matrix into the slot at byte offset `slot_off`. The descriptor starts at
-  // the tile's first key and ends at the slice's end, so the rows past a short last tile read as
-  // zeros (their scores are masked; zero V rows add nothing); tt >= ntiles issues the same pieces
-  // through a zero-extent descriptor (no access), so every vmcnt count is a constant.
-  auto issue = [&](int tt, int blk_raw, int slot_off) __attribute__((always_inline)) {
+  // Descriptor of tile tt of this wave's matrix: it starts at the tile's first key and ends at the
+  // slice's end, so the rows past a short last tile read as zeros (their scores are masked; zero V
+  // rows add nothing); tt >= ntiles gives a zero-extent descriptor (no access, same vmcnt count).
+  auto tile_srd = [&](int tt, int blk_raw) __attribute__((always_inline)) -> srd_t {
     const int blk = __builtin_amdgcn_readfirstlane(blk_raw);
-    const bool pooled = tt >= ntm;
     int kstart = blk * kQBlk + (tt & 1) * kKT;
     const uint8_t* base = my_mbase;
     int bytes = main_bytes;
-    if (pooled) {
+    if (tt >= ntm) {
       kstart = (tt - ntm) * kKT;
       base = my_pbase;
       bytes = pool_bytes;
     }
     const int soff = kstart * my_rowb;
-    bytes = tt >= ntiles ? 0 : bytes - soff;
-    const srd_t sd{base + soff, bytes};
+    return srd_t{base + soff, tt >= ntiles ? 0 : bytes - soff};
+  };
+  auto issue = [&](int tt, int blk_raw, int slot_off) __attribute__((always_inline)) {
+    const srd_t sd = tile_srd(tt, blk_raw);
     uint8_t* dst = smem + slot_off + sub * kPieces * 1024;
 #pragma unroll
     for (int i = 0; i < kPieces; ++i) dma16(sd, dst + i * 1024, vo[i], 0);
   };
-  auto blk_of = [&](int tt) __attribute__((always_inline)) -> int {
-    return (int)list[min(max(tt, 0) >> 1, kMaxBlocks - 1)];
+  // the slots DMA-filled in iteration t: K(t+R) into K(t)'s, V(t+R-1) into V(t-1)'s
+  auto dma_slot_off = [&](int t) __attribute__((always_inline)) -> int {
+    return my_mat == 0 ? (t % kRing) * kMatBytes : kVBase + ((t + kRing - 1) % kRing) * kMatBytes;
   };
+  const bool dma_wave = kProd ? producer : true;
+  // LDS address of this wave's pieces within a slot of its matrix's ring
+  const uint32_t dma_wave_base = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)smem)) +
+      (my_mat == 0 ? 0 : kVBase) + sub * kPieces * 1024);
+
+  // ---- prologue DMA: K(0..R-1), V(0..R-2) ---------------------------------------------------------
+  if (dma_wave) {
+    if (my_mat == 0) {
+#pragma unroll
+      for (int i = 0; i < kRing; ++i) issue(i, blk_of(i), i * kMatBytes);
+      VB_WAIT_VMCNT((kRing - 1) * kPieces);   // K(0) landed
+    } else {
+#pragma unroll
+      for (int i = 0; i < kRing - 1; ++i) issue(i, blk_of(i), kVBase + i * kMatBytes);
+    }
+  }
+
+  if constexpr (kProd) {
+    if (producer) {
+      // The producer's whole program: one barrier per tile, matching the compute waves', then the
+      // next tile's pieces into the slot that barrier freed.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      int blk_next = blk_of(kRing - my_mat);
+      for (int t = 0; t < ntiles; ++t) {
+        VB_WAIT_VMCNT((kRing - 2) * kPieces);   // K(t+1) / V(t) landed
+        const int blk = blk_next;
+        blk_next = blk_of(t + kRing + 1 - my_mat);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (!VB_FWD1_NODMA) issue(t + kRing - my_mat, blk, dma_slot_off(t));
+      }
+      VB_WAIT_VMCNT(0);
+      return;
+    }
+  }
+
+  // ======================================== compute waves ==========================================
   // valid keys of tile tt (64 unless it is the short last tile of the main or pooled keys)
   auto klen_of = [&](int tt, int blk_raw) __attribute__((always_inline)) -> int {
     const int blk = __builtin_amdgcn_readfirstlane(blk_raw);
     return tt >= ntm ? min(kKT, p.Lkp - (tt - ntm) * kKT) : min(kKT, Lk - (blk * kQBlk + (tt & 1) * kKT));
   };
-
-  // ---- per-lane LDS read addresses (loop-invariant; slots are immediates) -------------------------
+  const uint32_t smem_u32 = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)smem));
   int k_lane[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) k_lane[ks] = k_off<D>(l32, 2 * ks + half);
@@ -277,7 +373,6 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) v_lane[dt] = smem_u32 + kVBase + v_off_bytes<D>(vrow, dt * 32 + vcol);
 
-  // ---- state ----------------------------------------------------------------------------------------
   f32x16 o[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i)
@@ -292,8 +387,6 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
   V8 pf01[2];                     // P(t) of keys 0..31
   s16x4 vlo01[2][DT], vhi01[2][DT];   // V(t)^T fragments of k-steps 0, 1
 #pragma unroll
-  for (int r = 0; r < 16; ++r) cb[r] = 0.f;
-#pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) pp[i][e] = T::from_f32(0.f);
@@ -303,20 +396,21 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
       for (int e = 0; e < 4; ++e) vlo23[i][dt][e] = vhi23[i][dt][e] = 0;
   }
 
-  auto read_k = [&](int kslot_off, int kt, V8* kf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(smem + kslot_off + kt * 32 * kRowB, k_lane[ks]);
+  // O += a . b; S = k . q + c; S += k . q (the register-split forms at D=128)
+  auto o_mma = [&](f32x16& acc, const V8& a, const V8& bb) __attribute__((always_inline)) {
+    if constexpr (kRegSplit) mfma_acc_a<T>(acc, a, bb);
+    else acc = T::mfma32(a, bb, acc);
   };
-  // V^T fragments of k-step kk (16 keys) of the V slot at `vslot_off` (relative to the V ring)
-  auto read_v = [&](int vslot_off, int kk, s16x4* lo, s16x4* hi) __attribute__((always_inline)) {
-    const int r0 = (kk >> 1) * 32 + 16 * (kk & 1);
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      lo[dt] = lds_tr4_asm(v_lane[dt], vslot_off + r0 * kRowB);
-      hi[dt] = lds_tr4_asm(v_lane[dt], vslot_off + (r0 + 8) * kRowB);
-    }
+  auto s_mma0 = [&](const V8& a, const V8& bq, const f32x16& c) __attribute__((always_inline)) -> f32x16 {
+    if constexpr (kRegSplit) return mfma_bq<T>(a, bq, c);
+    else return T::mfma32(a, bq, c);
   };
-  // P = exp2(S) of one 32-key half packed to the storage type; returns the lane's fp32 sum
+  auto s_mma = [&](f32x16& acc, const V8& a, const V8& bq) __attribute__((always_inline)) {
+    if constexpr (kRegSplit) mfma_bq_acc<T>(acc, a, bq);
+    else acc = T::mfma32(a, bq, acc);
+  };
+  // P = exp2(S) of one 32-key half packed to the storage type; returns the lane's fp32 sum (the
+  // slow path's recomputation; the placed loop below spreads the same arithmetic over the gaps)
   auto exp_pack = [&](const f32x16& x, V8& p0, V8& p1) __attribute__((always_inline)) -> float {
     float e[16];
     float h4[4];
@@ -345,60 +439,6 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
     for (int r = 0; r < 16; ++r)
       if (kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half >= klen) x[r] = -INFINITY;
   };
-  auto bias_of = [&](int tt) __attribute__((always_inline)) -> float {
-    return (kPool && tt >= ntm) ? p.pool_bias_l2 : 0.f;
-  };
-
-#if VB_DIAG
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-  F1_STAMP(p0);
-  // ---- prologue: K(0..R-1), V(0..R-2) in flight; S(0) and the first tile's exact max -------------
-  {
-    const int b0 = blk_of(0);
-    if (my_mat == 0) {
-#pragma unroll
-      for (int i = 0; i < kRing; ++i) issue(i, blk_of(i), i * kMatBytes);
-      VB_WAIT_VMCNT((kRing - 1) * kPieces);
-    } else {
-#pragma unroll
-      for (int i = 0; i < kRing - 1; ++i) issue(i, blk_of(i), kVBase + i * kMatBytes);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const float bias0 = bias_of(0);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) cb[r] = bias0;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      V8 kf[KS];
-      read_k(0, kt, kf);
-      s[0][kt] = T::mfma32(kf[0], qf[0], cb);
-#pragma unroll
-      for (int ks = 1; ks < KS; ++ks) s[0][kt] = T::mfma32(kf[ks], qf[ks], s[0][kt]);
-    }
-    const int kl0 = klen_of(0, b0);
-    if (kl0 < kKT) {
-      asm volatile("");
-      mask_tail(s[0][0], 0, kl0);
-      mask_tail(s[0][1], 1, kl0);
-    }
-    const float mt = max_xor32(fmaxf(half_max(s[0][0]), half_max(s[0][1])));
-    m = mt;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[0][0][r] -= mt;
-      s[0][1][r] -= mt;
-      cb[r] -= mt;
-    }
-  }
-  F1_STAMP(p1);
-  F1_ACC(4, p1 - p0);
-  // carried list entries: the block of tile t+1 (its klen) and of this wave's next DMA tile
-  int blk_s1 = blk_of(1);
-  int blk_dma = blk_of(kRing - my_mat);
-
   // raise m by delta (> 0 somewhere): rescale O, l, the seed and the three S registers still at
   // the old max
   auto raise_m = [&](float mt_half, f32x16& r0, f32x16& r1, f32x16& r2) __attribute__((always_inline)) {
@@ -419,168 +459,92 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
     }
   };
 
-  // ---- one tile: iteration t, compile-time slot phase U = t % 6 ------------------------------------
-  auto body = [&](int t, auto U) __attribute__((always_inline)) {
-    constexpr int u = decltype(U)::value;
-    constexpr int cur = u & 1, nxt = cur ^ 1;          // S buffers of tiles t and t+1
-    constexpr int kSlotK1 = ((u + 1) % kRing) * kMatBytes;               // K(t+1)
-    constexpr int kSlotV = (u % kRing) * kMatBytes;                      // V(t), relative to kVBase
-    // K waves: K(t+1) landed (K(t+2) .. K(t+R-1) younger); V waves: V(t) landed (V(t+1) ..
-    // V(t+R-2) younger)
-    F1_STAMP(b0);
-    VB_WAIT_VMCNT((kRing - 2) * kPieces);
-    lgkm_wait(vlo23, vhi23);
+#if VB_DIAG
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  F1_STAMP(p0);
+  // ---- prologue: S(0) and the first tile's exact max ---------------------------------------------
+  {
+    const int b0 = blk_of(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    F1_STAMP(b1);
-    F1_ACC(0, b1 - b0);
-
-    // ======== region A ========
-    V8 kf0[KS], kf1[KS];
-    read_k(kSlotK1, 0, kf0);
-    // P(t-1) . V(t-1), k-steps 2 and 3
+    const float bias0 = (kPool && ntm == 0) ? p.pool_bias_l2 : 0.f;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int r = 0; r < 16; ++r) cb[r] = bias0;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo23[kk][dt], vhi23[kk][dt]), pp[kk], o[dt]);
-    read_k(kSlotK1, 1, kf1);
-    // S(t+1), keys 0..31
-    s[nxt][0] = T::mfma32(kf0[0], qf[0], cb);
+    for (int kt = 0; kt < 2; ++kt) {
+      V8 kf[KS];
 #pragma unroll
-    for (int ks = 1; ks < KS; ++ks) s[nxt][0] = T::mfma32(kf0[ks], qf[ks], s[nxt][0]);
-    read_v(kSlotV, 0, vlo01[0], vhi01[0]);
-    read_v(kSlotV, 1, vlo01[1], vhi01[1]);
-    // LDS-DMA (after this region's reads in program order: the DMA writes LDS): K(t+R) into
-    // K(t)'s slot, or V(t+R-1) into V(t-1)'s slot
-    {
-      const int tt = t + kRing - my_mat;
-      const int slot_off = my_mat == 0 ? (u % kRing) * kMatBytes : kVBase + ((u + kRing - 1) % kRing) * kMatBytes;
-      issue(tt, blk_dma, slot_off);
+      for (int ks = 0; ks < KS; ++ks) kf[ks] = lds_b128<T>(smem + kt * 32 * kRowB, k_lane[ks]);
+      s[0][kt] = s_mma0(kf[0], qf[0], cb);
+#pragma unroll
+      for (int ks = 1; ks < KS; ++ks) s_mma(s[0][kt], kf[ks], qf[ks]);
     }
-    float hs0 = exp_pack(s[cur][0], pf01[0], pf01[1]);
-    asm volatile("" : "+v"(pf01[0]), "+v"(pf01[1]));   // packs stay in the region (not sunk past the check)
-#if VB_FWD1_SCHED
-    // 2*DT + KS MFMAs, each with its share of the exp/pack VALU: the LDS reads in the first half
-    // of the gaps (the K reads feed this region's S MFMAs), the DMA pieces in the second half
-    {
-      constexpr int nM = 2 * DT + KS;
-      constexpr int nDS = 2 * KS + 4 * DT;
-#pragma unroll
-      for (int i = 0; i < nM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(kMaskMFMA, 1, 0);
-        if (i < nM / 2) __builtin_amdgcn_sched_group_barrier(kMaskDSR, nDS / (nM / 2), 0);
-        __builtin_amdgcn_sched_group_barrier(kMaskVALU, D == 64 ? 5 : 3, 0);
-        if (i >= nM / 2) __builtin_amdgcn_sched_group_barrier(kMaskVMEM, (2 * kPieces) / nM, 0);
-      }
-    }
-#endif
-    if (!__all(hs0 <= kLazyBound)) {
+    if constexpr (kRegSplit) hazard_pad(o, s[0][0], s[0][1], cb);
+    const int kl0 = klen_of(0, b0);
+    if (kl0 < kKT) {
       asm volatile("");
-      raise_m(half_max(s[cur][0]), s[cur][0], s[cur][1], s[nxt][0]);
-      hs0 = exp_pack(s[cur][0], pf01[0], pf01[1]);
+      mask_tail(s[0][0], 0, kl0);
+      mask_tail(s[0][1], 1, kl0);
     }
-    l += hs0;
-    F1_STAMP(b2);
-    F1_ACC(1, b2 - b1);
-
-    // ======== region B ========
-    lgkm_wait(vlo01, vhi01);
-    // S(t+1), keys 32..63
-    s[nxt][1] = T::mfma32(kf1[0], qf[0], cb);
+    const float mt = max_xor32(fmaxf(half_max(s[0][0]), half_max(s[0][1])));
+    m = mt;
 #pragma unroll
-    for (int ks = 1; ks < KS; ++ks) s[nxt][1] = T::mfma32(kf1[ks], qf[ks], s[nxt][1]);
-    // P(t) . V(t), k-steps 0 and 1
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo01[kk][dt], vhi01[kk][dt]), pf01[kk], o[dt]);
-    // V(t) fragments of k-steps 2, 3 for the next iteration; list entries for it
-    read_v(kSlotV, 2, vlo23[0], vhi23[0]);
-    read_v(kSlotV, 3, vlo23[1], vhi23[1]);
-    const int blk_s2 = blk_of(t + 2);
-    const int blk_dma_next = blk_of(t + kRing + 1 - my_mat);
-    float hs1 = exp_pack(s[cur][1], pp[0], pp[1]);
-    asm volatile("" : "+v"(pp[0]), "+v"(pp[1]));
-#if VB_FWD1_SCHED
-    {
-      constexpr int nM = 2 * DT + KS;
-      constexpr int nDS = 4 * DT + 2;
-#pragma unroll
-      for (int i = 0; i < nM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(kMaskMFMA, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(kMaskDSR, (nDS + nM - 1) / nM, 1);
-        __builtin_amdgcn_sched_group_barrier(kMaskVALU, D == 64 ? 5 : 3, 1);
-      }
+    for (int r = 0; r < 16; ++r) {
+      s[0][0][r] -= mt;
+      s[0][1][r] -= mt;
+      cb[r] -= mt;
     }
-#endif
-    if (!__all(hs1 <= kLazyBound)) {
-      asm volatile("");
-      raise_m(half_max(s[cur][1]), s[cur][1], s[nxt][0], s[nxt][1]);
-      hs1 = exp_pack(s[cur][1], pp[0], pp[1]);
-    }
-    l += hs1;
-    F1_STAMP(b3);
-    F1_ACC(2, b3 - b2);
-    // S(t+1): a short tile's missing keys; the seed of S(t+2) when its key source changes
-    const int kl1 = klen_of(t + 1, blk_s1);
-    if (kl1 < kKT) {
-      asm volatile("");
-      mask_tail(s[nxt][0], 0, kl1);
-      mask_tail(s[nxt][1], 1, kl1);
-    }
-    if constexpr (kPool) {
-      if (t + 2 == ntm) {   // tile t+2 is the first pooled tile: seed += the pooled keys' bias
-        asm volatile("");
+    if (kPool && ntm == 1) {   // tile 1 is the first pooled tile: the seed of S(1) carries the bias
 #pragma unroll
-        for (int r = 0; r < 16; ++r) cb[r] += p.pool_bias_l2;
-      }
+      for (int r = 0; r < 16; ++r) cb[r] += p.pool_bias_l2;
     }
-    blk_s1 = blk_s2;
-    blk_dma = blk_dma_next;
-    F1_STAMP(b4);
-    F1_ACC(3, b4 - b3);
-  };
-
-  if (kPool && ntm == 1) {   // tile 1 is the first pooled tile: the seed of S(1) carries the bias
-#pragma unroll
-    for (int r = 0; r < 16; ++r) cb[r] += p.pool_bias_l2;
   }
-  // ---- the same iteration with every instruction group placed by hand ---------------------------
+  F1_STAMP(p1);
+  F1_ACC(4, p1 - p0);
+  // carried list entries: the block of tile t+1 (its klen) and of this wave's next DMA tile
+  int blk_s1 = blk_of(1);
+  int blk_dma = kProd ? 0 : blk_of(kRing - my_mat);
+
+  // ---- iteration t, compile-time phase U = t % kPeriod ---------------------------------------------
   // Each MFMA gets a fixed set of fillers, pinned by sched_barrier: the exps of S(t) spread evenly
   // (16 per region), each exp's row-sum add and the bf16 pack of each finished pair one gap later
   // (off the exp's latency), the LDS reads of the operands two or more gaps before their MFMA, and
   // the LDS-DMA pieces in the gaps after the region's reads (the DMA writes LDS; it goes last).
-  auto body_placed = [&](int t, auto U) __attribute__((always_inline)) {
+  auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
     constexpr int cur = u & 1, nxt = cur ^ 1;
     constexpr int kSlotK1 = ((u + 1) % kRing) * kMatBytes;
     constexpr int kSlotV = (u % kRing) * kMatBytes;
-    constexpr int nA = 2 * DT + KS;      // MFMAs per region (the same count in both)
-    constexpr int epg = 16 / nA;         // exps per gap: 2 at D=64, 1 at D=128
     F1_STAMP(b0);
-    VB_WAIT_VMCNT((kRing - 2) * kPieces);
+    if constexpr (!kProd) VB_WAIT_VMCNT((kRing - 2) * kPieces);   // K(t+1) / V(t) landed
     lgkm_wait(vlo23, vhi23);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     F1_STAMP(b1);
     F1_ACC(0, b1 - b0);
-    // this iteration's DMA descriptor (scalar work, before the MFMA stream)
-    const int tt = t + kRing - my_mat;
-    const int slot_off = my_mat == 0 ? (u % kRing) * kMatBytes : kVBase + ((u + kRing - 1) % kRing) * kMatBytes;
-    const int blk = __builtin_amdgcn_readfirstlane(blk_dma);
-    const bool pooled = tt >= ntm;
-    int kstart = blk * kQBlk + (tt & 1) * kKT;
-    const uint8_t* dbase = my_mbase;
-    int dbytes = main_bytes;
-    if (pooled) {
-      kstart = (tt - ntm) * kKT;
-      dbase = my_pbase;
-      dbytes = pool_bytes;
+    srd_t sd{nullptr, 0};
+    uint32_t dma_dst = 0;
+    if constexpr (!kProd) {   // this iteration's DMA descriptor (scalar work, before the MFMA stream)
+      sd = tile_srd(t + kRing - my_mat, blk_dma);
+      // LDS address of this wave's first piece: an opaque scalar, so each piece's M0 is one s_add
+      // of an immediate (hipcc would otherwise keep every slot x piece address in an SGPR)
+      dma_dst = dma_wave_base + (my_mat == 0 ? (u % kRing) * kMatBytes : ((u + kRing - 1) % kRing) * kMatBytes);
+#if __HIP_DEVICE_COMPILE__   // "s" (an SGPR) is no constraint on the host target
+      asm volatile("" : "+s"(dma_dst));
+#endif
     }
-    const int soff = kstart * my_rowb;
-    dbytes = tt >= ntiles ? 0 : dbytes - soff;
-    const srd_t sd{dbase + soff, dbytes};
-    uint8_t* dma_dst = smem + slot_off + sub * kPieces * 1024;
+    // piece i of this iteration's DMA (half of them in each region, one every `step` gaps)
+    auto dma_piece = [&](int i) __attribute__((always_inline)) {
+#if __HIP_DEVICE_COMPILE__   // an integer-to-LDS-pointer cast has no host meaning (the host pass would drop the stub)
+      if (!VB_FWD1_NODMA)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(sd.base), (short)0, sd.bytes, 0x00020000),
+            (__attribute__((address_space(3))) void*)(uintptr_t)(dma_dst + i * 1024), 16, vo[i], 0, 0, 0);
+#endif
+    };
+    constexpr int step = 2 * nA / kPieces;
     __builtin_amdgcn_sched_barrier(0);
 
     V8 kf0[KS], kf1[KS];
@@ -591,12 +555,12 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 #pragma unroll
       for (int j = 0; j < epg; ++j) {
         const int r = g * epg + j;
-        if (r < 16) e[r] = exp2_fast(x[r]);
+        if (r < 16) e[r] = (VB_FWD1_ABL & 2) ? x[r] : exp2_fast(x[r]);
       }
 #pragma unroll
       for (int j = 0; j < epg; ++j) {
         const int r = (g - 1) * epg + j;
-        if (r >= 0 && r < 16) {
+        if (r >= 0 && r < 16 && !(VB_FWD1_ABL & 4)) {
           if (r < 4) h4[r] = e[r];
           else h4[r & 3] += e[r];
           if (r & 1) {
@@ -613,15 +577,15 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 #pragma unroll
       for (int j = 0; j < epg; ++j) {
         const int r = (nA - 1) * epg + j;
+        if (VB_FWD1_ABL & 4) {
+          if (r < 4) h4[r] = e[r];
+          continue;
+        }
         if (r >= 4 && r < 16) h4[r & 3] += e[r];
         if (r < 16 && (r & 1)) {
           pk[r >> 3][(r & 7) >> 1] = pack2<T>(e[r - 1], e[r]);
           asm volatile("" : "+v"(pk[r >> 3][(r & 7) >> 1]));
         }
-      }
-#pragma unroll
-      for (int r = nA * epg; r < 16; ++r) {   // exps that did not fit the gaps (none at 16 / nA)
-        e[r] = exp2_fast(s[cur][0][r]);
       }
       p0 = __builtin_bit_cast(V8, pk[0]);
       p1 = __builtin_bit_cast(V8, pk[1]);
@@ -633,10 +597,11 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
     for (int g = 0; g < nA; ++g) {
       if (g < 2 * DT) {
         const int kk = g / DT, dt = g % DT;
-        o[dt] = T::mfma32(join8<T>(vlo23[kk][dt], vhi23[kk][dt]), pp[kk], o[dt]);
+        o_mma(o[dt], join8<T>(vlo23[kk][dt], vhi23[kk][dt]), pp[kk]);
       } else {
         const int ks = g - 2 * DT;
-        s[nxt][0] = T::mfma32(kf0[ks], qf[ks], ks == 0 ? cb : s[nxt][0]);
+        if (ks == 0) s[nxt][0] = s_mma0(kf0[ks], qf[ks], cb);
+        else s_mma(s[nxt][0], kf0[ks], qf[ks]);
       }
       __builtin_amdgcn_sched_barrier(0);   // the MFMA opens its gap
       fill(s[cur][0], g);
@@ -644,6 +609,11 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int d = 2 * g + j;
+        if (VB_FWD1_ABL & 1) {
+          if (d < KS) kf0[d] = qf[d];
+          else if (d < 2 * KS) kf1[d - KS] = qf[d - KS];
+          continue;
+        }
         if (d < KS) kf0[d] = lds_b128<T>(smem + kSlotK1, k_lane[d]);
         else if (d < 2 * KS) kf1[d - KS] = lds_b128<T>(smem + kSlotK1 + 32 * kRowB, k_lane[d - KS]);
         else if (d < 2 * KS + 4 * DT) {
@@ -655,18 +625,17 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
           else vlo01[kk][dt] = x;
         }
       }
-      // LDS-DMA pieces, one per gap, in the gaps after the reads
-      {
-        const int i = g - (nA - kPieces);
-        if (i >= 0 && i < kPieces && !VB_FWD1_NODMA) dma16(sd, dma_dst + i * 1024, vo[i], 0);
-      }
+      if constexpr (!kProd)
+        if (g % step == 1) dma_piece(g / step);
       __builtin_amdgcn_sched_barrier(0);
     }
     float hs0 = finish(pf01[0], pf01[1]);
     if (!__all(hs0 <= kLazyBound)) {
       asm volatile("");
+      if constexpr (kRegSplit) hazard_pad(o, s[nxt][0], s[cur][0], cb);
       raise_m(half_max(s[cur][0]), s[cur][0], s[cur][1], s[nxt][0]);
       hs0 = exp_pack(s[cur][0], pf01[0], pf01[1]);
+      if constexpr (kRegSplit) hazard_pad(o, s[nxt][0], s[cur][1], cb);
     }
     l += hs0;
     F1_STAMP(b2);
@@ -677,18 +646,21 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 #pragma unroll
     for (int g = 0; g < nA; ++g) {
       if (g < KS) {
-        s[nxt][1] = T::mfma32(kf1[g], qf[g], g == 0 ? cb : s[nxt][1]);
+        if (g == 0) s[nxt][1] = s_mma0(kf1[g], qf[g], cb);
+        else s_mma(s[nxt][1], kf1[g], qf[g]);
       } else {
         if (g == KS) lgkm_wait(vlo01, vhi01);   // region A's V reads (no region-B read is older)
         const int kk = (g - KS) / DT, dt = (g - KS) % DT;
-        o[dt] = T::mfma32(join8<T>(vlo01[kk][dt], vhi01[kk][dt]), pf01[kk], o[dt]);
+        o_mma(o[dt], join8<T>(vlo01[kk][dt], vhi01[kk][dt]), pf01[kk]);
       }
       __builtin_amdgcn_sched_barrier(0);
       fill(s[cur][1], g);
+      if constexpr (!kProd)
+        if (g % step == 1) dma_piece(kPieces / 2 + g / step);
       if (g == 0) blk_s2 = blk_of(t + 2);
-      if (g == 1) blk_dma_next = blk_of(t + kRing + 1 - my_mat);
+      if (!kProd && g == 1) blk_dma_next = blk_of(t + kRing + 1 - my_mat);
       // V(t) k-steps 2, 3 for the next iteration, after the P.V MFMAs started (two per gap)
-      if (g >= KS) {
+      if (g >= KS && !(VB_FWD1_ABL & 1)) {
 #pragma unroll
         for (int j = 0; j < 4 * DT / (nA - KS); ++j) {
           const int v = (g - KS) * (4 * DT / (nA - KS)) + j;
@@ -704,23 +676,28 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
     float hs1 = finish(pp[0], pp[1]);
     if (!__all(hs1 <= kLazyBound)) {
       asm volatile("");
+      if constexpr (kRegSplit) hazard_pad(o, s[nxt][0], s[nxt][1], cb);
       raise_m(half_max(s[cur][1]), s[cur][1], s[nxt][0], s[nxt][1]);
       hs1 = exp_pack(s[cur][1], pp[0], pp[1]);
+      if constexpr (kRegSplit) hazard_pad(o, s[nxt][0], s[nxt][1], cb);
     }
     l += hs1;
     F1_STAMP(b3);
     F1_ACC(2, b3 - b2);
+    // S(t+1): a short tile's missing keys; the seed of S(t+2) when its key source changes
     const int kl1 = klen_of(t + 1, blk_s1);
     if (kl1 < kKT) {
       asm volatile("");
+      if constexpr (kRegSplit) hazard_pad(o, s[nxt][0], s[nxt][1], cb);
       mask_tail(s[nxt][0], 0, kl1);
       mask_tail(s[nxt][1], 1, kl1);
     }
     if constexpr (kPool) {
-      if (t + 2 == ntm) {
+      if (t + 2 == ntm) {   // tile t+2 is the first pooled tile: seed += the pooled keys' bias
         asm volatile("");
 #pragma unroll
         for (int r = 0; r < 16; ++r) cb[r] += p.pool_bias_l2;
+        if constexpr (kRegSplit) hazard_pad(o, s[nxt][0], s[nxt][1], cb);
       }
     }
     blk_s1 = blk_s2;
@@ -731,10 +708,7 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 
   // the body instantiated once per (ring slot, S parity) phase: every LDS offset an immediate
   auto run_phase = [&](int t0, auto U) __attribute__((always_inline)) {
-    if (t0 + decltype(U)::value < ntiles) {
-      if constexpr (VB_FWD1_SCHED == 2) body_placed(t0 + decltype(U)::value, U);
-      else body(t0 + decltype(U)::value, U);
-    }
+    if (t0 + decltype(U)::value < ntiles) body(t0 + decltype(U)::value, U);
   };
   for (int t0 = 0; t0 < ntiles; t0 += kPeriod)
     for_phases([&](auto U) __attribute__((always_inline)) { run_phase(t0, U); },
@@ -744,8 +718,9 @@ __global__ void __launch_bounds__(kThreads, kOcc) attn_fwd1_kernel(const FwdPara
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] = T::mfma32(join8<T>(vlo23[kk][dt], vhi23[kk][dt]), pp[kk], o[dt]);
-  VB_WAIT_VMCNT(0);   // the zero-extent DMAs issued past the last tile retire before exit
+    for (int dt = 0; dt < DT; ++dt) o_mma(o[dt], join8<T>(vlo23[kk][dt], vhi23[kk][dt]), pp[kk]);
+  if constexpr (kRegSplit) hazard_pad(o, s[0][0], s[0][1], cb);   // the epilogue's VALU reads O
+  if constexpr (!kProd) VB_WAIT_VMCNT(0);   // the zero-extent DMAs issued past the last tile retire
   F1_STAMP(e0);
 
   // ---- epilogue (attn_fwd_kernel's: 16-byte row stores through permlane32_swap) -------------------
@@ -787,8 +762,10 @@ template <int D, class T>
 static int launch_fwd1_t(const FwdParams& p, bool pool, hipStream_t stream) {
   const dim3 grid(p.nbq * p.B * p.H);
   constexpr int occ = D == 64 ? VB_FWD1_OCC64 : 1;
-  if (pool) hipLaunchKernelGGL((attn_fwd1_kernel<D, T, true, occ>), grid, dim3(kThreads), 0, stream, p);
-  else hipLaunchKernelGGL((attn_fwd1_kernel<D, T, false, occ>), grid, dim3(kThreads), 0, stream, p);
+  constexpr bool prod = D == 64 && VB_FWD1_PROD64;
+  const dim3 block(prod ? 2 * kThreads : kThreads);
+  if (pool) hipLaunchKernelGGL((attn_fwd1_kernel<D, T, true, occ, prod>), grid, block, 0, stream, p);
+  else hipLaunchKernelGGL((attn_fwd1_kernel<D, T, false, occ, prod>), grid, block, 0, stream, p);
   return check_launch("attn_fwd1_kernel");
 }
 
