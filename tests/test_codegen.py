@@ -75,3 +75,42 @@ def test_makefile_falls_back_when_the_scheduler_option_is_gone():
     bad = subprocess.run(["make", "-C", mk, "-n", "-B", "ILP_FLAG=-mllvm -amdgpu-no-such-option=1",
                           os.path.join(mk, "build", "vb_attn_fwd.hip.o")], capture_output=True, text=True)
     assert bad.returncode == 0 and "rejects" in bad.stderr and "no-such-option" not in bad.stdout
+
+
+# ---- the hand-scheduled D=128 dK/dV (vb_attn_bwd_kv128.hip) ---------------------------------------
+# Its LDS operands are read by inline asm and waited for with lgkmcnt counts derived from the
+# schedule, invisible to hipcc: a register spill or copy of an asm-read value before its wait, or a
+# miscounted wait, would read stale data. tools/diag/lgkm_check.py models the LDS counter over the
+# ISA and reports any such use.
+KV128_SRC = os.path.join(ROOT, "video-blade_amd", "csrc", "vb_attn_bwd_kv128.hip")
+KV128_KERNELS = [f"_ZN2vb18bwd_dkdv128_kernelINS_{t}ELb{p}EEEvNS_9BwdParamsE"
+                 for t in ("4BF16", "3F16") for p in (0, 1)]
+
+
+@pytest.fixture(scope="module")
+def kv128_asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("asm") / "kv128.s"
+    cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "video-blade_amd", "csrc"),
+           "--cuda-device-only", "-S", KV128_SRC, "-o", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True)
+    return str(out)
+
+
+@pytest.mark.parametrize("name", KV128_KERNELS)
+def test_kv128_lds_waits_cover_every_use(kv128_asm, name, capsys):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools", "diag"))
+    import lgkm_check
+    assert lgkm_check.check(kv128_asm, name) == 0, capsys.readouterr().out[-2000:]
+
+
+@pytest.mark.parametrize("name", KV128_KERNELS)
+def test_kv128_no_spills(kv128_asm, name):
+    text = open(kv128_asm).read()
+    i = text.index(f".name:           {name}")
+    meta = text[i:i + 600]   # the fields follow .name in the kernel's metadata block
+    assert re.search(r"\.vgpr_spill_count:\s+0\b", meta), "VGPR spills in " + name
+    assert re.search(r"\.private_segment_fixed_size:\s+0\b", meta), "scratch in " + name

@@ -114,8 +114,10 @@ def main():
                     else:
                         same = all(torch.equal(o, r) for o, r in zip(outs, ref))
                         err = max((o.float() - r.float()).abs().max().item() for o, r in zip(outs, ref))
+                        rel = ", ".join(f"{(o.float() - r.float()).abs().max().item() / max(r.float().abs().max().item(), 1e-30):.2e}"
+                                        for o, r in zip(outs, ref))
                         print(f"  {t}: bit-identical to {a.tags[0]} over {len(outs)} output(s): {same}; "
-                              f"max|diff| = {err:.3e}")
+                              f"max|diff| = {err:.3e}; per output max|diff|/max|ref| = {rel}")
             for _ in range(a.rounds):
                 for kk, t in zip(keys, a.tags):
                     _lib._lib = libs[t]

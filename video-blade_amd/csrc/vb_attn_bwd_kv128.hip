@@ -1,0 +1,643 @@
+// dK / dV of the block-sparse FMHA backward at head_dim 128, hand-scheduled for gfx950 (MI355X).
+//
+// Same work items, operand maps, math and outputs as bwd_dkdv_kernel<128> (vb_attn_bwd.hip; the
+// reference's backward semantics are described there): one workgroup per (b, h, 128-key block),
+// wave = 32 keys, the 64-row Q / dO / stats tiles of the q-blocks that keep the key block streamed
+// through LDS by LDS-DMA. What differs is the schedule. bwd_dkdv_kernel<128> runs one wave per SIMD
+// (its registers allow no more) and leaves each step's latency exposed: S/dP MFMAs, then the
+// exp/dS VALU with the MFMA pipe idle, then the dV/dK MFMAs, every LDS read waited for right
+// before its MFMA (profiles/r04_pmc_bwd_wan.txt: MFMA busy 0.30).
+//
+// Here every wave runs one fixed stream of 64 MFMAs per tile t, in four sections of 16:
+//   A = X(t,0)   S = Q.K^T and dP = dO.V^T of rows 0-31 (two interleaved chains)
+//   B = Y(t-1,1) dV += dO^T.P, dK += Q^T.dS of the previous tile's rows 32-63
+//   C = X(t,1)   rows 32-63
+//   D = Y(t,0)   rows 0-31
+// and places all other work in the gaps between the MFMAs (one gap per MFMA, pinned with
+// sched_barrier): the exp / dS / pack arithmetic of X(t,0) spread over gaps 18-47 and of X(t,1)
+// over gaps 50-63 and 0-15 of the next tile (64 VALU each, about two per gap); every MFMA's LDS
+// operand read issued kLA gaps ahead (asm reads, waited with exact lgkmcnt counts derived from
+// the schedule below); the tile's row statistics; the barrier (gap 52) and the nine LDS-DMA
+// pieces of tile t+3 (gaps 52-60) into a 4-slot ring. K and V (the B operands of X) and the dK/dV
+// accumulators live in AGPRs; all MFMAs are asm (v_mfma_f32_32x32x16), preceded by s_nop 1 for
+// the VALU-write -> MFMA-read wait states the compiler cannot see.
+#include <cstdlib>
+#include <type_traits>
+#include <utility>
+
+#include "vb_attn_bwd.hpp"
+
+#ifndef VB_BWD_KV128_DEFAULT
+#define VB_BWD_KV128_DEFAULT 1
+#endif
+#ifndef VB_KV128_LA
+#define VB_KV128_LA 4      // operand lookahead in MFMAs
+#endif
+
+namespace vb {
+namespace kv128 {
+
+constexpr int kLA = VB_KV128_LA;
+static_assert(kLA >= 2 && kLA <= 4, "lookahead out of range (the next tile's operands are read in gaps 53-56)");
+// LDS map (bytes): Q ring 4 x 16 KiB, dO ring 4 x 16 KiB, stats ring 4 x 1 KiB, the 1 KiB sink of
+// the waves' padding DMA piece, the q-block list
+constexpr int kQOff = 0;
+constexpr int kDOOff = 65536;
+constexpr int kStOff = 131072;
+constexpr int kSinkOff = kStOff + 4096;
+constexpr int kListOff = kSinkOff + 1024;
+constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16;
+constexpr int kPieces = 9;   // LDS-DMA pieces per wave and tile: 4 of Q, 4 of dO, stats (wave 0) or sink
+constexpr int kGb = 52;      // gap of the tile barrier; DMA pieces in gaps kGb .. kGb + 8
+constexpr int kV0 = 18;      // V(t,0): gaps 18..47
+constexpr int kV1 = 50;      // V(t,1): gaps 50..63, then 0..15 of the next tile
+constexpr int kVGaps = 30;
+
+// ---- the LDS read schedule (drives both the issue and the lgkmcnt of every wait) ----------------
+// gap h issues, in order: the operand reads of MFMA h + kLA (X: one ds_read_b128; Y: two
+// ds_read_b64_tr_b16), unless h + kLA >= 64; then the extra reads of extra_reads(h):
+//   8, 9  L' of rows 0-31 (two f32x4 each)         24, 25  -Delta of rows 32-63 (dP seeds)
+//   40, 41 L' of rows 32-63                        42      the q-block of tile t+3 (list entry)
+//   53, 54 -Delta of tile t+1's rows 0-31 + the operand of its MFMA 0 / 1
+//   55, 56 the operands of tile t+1's MFMAs 2 / 3
+constexpr int op_reads(int g) { return ((g >> 4) & 1) ? 2 : 1; }
+constexpr int extra_reads(int h) {
+  return (h == 8 || h == 9 || h == 24 || h == 25 || h == 40 || h == 41) ? 2
+         : (h == 53 || h == 54) ? 2 + (h - 53 < kLA)
+         : (h == 55 || h == 56) ? (h - 53 < kLA)
+         : h == 42 ? 1 : 0;
+}
+constexpr int gap_reads(int h) { return (h + kLA < 64 ? op_reads(h + kLA) : 0) + extra_reads(h); }
+// lgkmcnt before MFMA g: the reads issued after g's operand (LDS returns in order); MFMAs
+// 0..kLA-1 read operands completed before the tile started
+constexpr int wait_n(int g) {
+  if (g < kLA) return 15;
+  int n = extra_reads(g - kLA);
+  for (int h = g - kLA + 1; h < g; ++h) n += gap_reads(h);
+  return n > 15 ? 15 : n;
+}
+static_assert(extra_reads(kGb) == 0 && extra_reads(kGb - 1) == 0, "no read beside the barrier");
+
+template <class F, int... Gs>
+__device__ __forceinline__ void for_gaps(F&& f, std::integer_sequence<int, Gs...>) {
+  (f(std::integral_constant<int, Gs>{}), ...);
+}
+
+// ---- asm building blocks (device pass only: the host pass has no VGPR/AGPR constraints) ----------
+template <class T>
+__device__ __forceinline__ void mf_zero(f32x16& d, const typename T::vec8& a, const typename T::vec8& b) {
+#if __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same<T, BF16>::value)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
+#endif
+}
+template <class T>
+__device__ __forceinline__ void mf_vacc(f32x16& d, const typename T::vec8& a, const typename T::vec8& b) {
+#if __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same<T, BF16>::value)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+#endif
+}
+template <class T>
+__device__ __forceinline__ void mf_aacc(f32x16& d, const typename T::vec8& a, const typename T::vec8& b) {
+#if __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same<T, BF16>::value)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
+#endif
+}
+template <int kImm, class V>
+__device__ __forceinline__ void rd128(V& r, uint32_t addr) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(kImm));
+#endif
+}
+template <int kImm>
+__device__ __forceinline__ void rdtr(s16x4& r, uint32_t addr) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(kImm));
+#endif
+}
+__device__ __forceinline__ void rdu16(uint32_t& r, uint32_t addr) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("ds_read_u16 %0, %1" : "=v"(r) : "v"(addr));
+#endif
+}
+template <int N, class V>
+__device__ __forceinline__ void wait1(V& a) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(N));
+#endif
+}
+template <int N>
+__device__ __forceinline__ void wait2(s16x4& a, s16x4& b) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
+#endif
+}
+// makes a value produced by an asm read usable only after the wait that preceded this statement
+template <class V>
+__device__ __forceinline__ void launder(V& a) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(a));
+#endif
+}
+template <class V>
+__device__ __forceinline__ void to_agpr(V& a) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+a"(a));
+#endif
+}
+
+// op k (0..63) of the score arithmetic of one 32-row half, in four stages of 16 so every op's
+// input was produced >= 7 gaps earlier:
+//   P = exp2(S c - L')   (fma, then exp, in place in s)
+//   dS = P * dP          (dp holds dO.V^T - Delta: seeded with -Delta)
+//   pp / pd = bf16 pairs of P / dS (the B operands of dV / dK)
+template <class T, int k>
+__device__ __forceinline__ void vop(f32x16& s, f32x16& dp, const f32x4 (&lq)[4], u32x4 (&pp)[2], u32x4 (&pd)[2],
+                                    float c) {
+  constexpr int st = k >> 4, r = k & 15;
+  if constexpr (st == 0) s[r] = fmaf(s[r], c, -lq[r >> 2][r & 3]);
+  else if constexpr (st == 1) s[r] = exp2_fast(s[r]);
+  else if constexpr (st == 2) dp[r] = dp[r] * s[r];
+  else if constexpr (r < 8) pp[r >> 2][r & 3] = pack2<T>(s[2 * r], s[2 * r + 1]);
+  else pd[(r - 8) >> 2][(r - 8) & 3] = pack2<T>(dp[2 * (r - 8)], dp[2 * (r - 8) + 1]);
+}
+template <class T, int i, int... Ks>
+__device__ __forceinline__ void vops_at(f32x16& s, f32x16& dp, const f32x4 (&lq)[4], u32x4 (&pp)[2],
+                                        u32x4 (&pd)[2], float c, std::integer_sequence<int, Ks...>) {
+  constexpr int lo = i * 64 / kVGaps;
+  (vop<T, lo + Ks>(s, dp, lq, pp, pd, c), ...);
+}
+// the ops of gap i (0..kVGaps-1) of a half's arithmetic
+template <class T, int i>
+__device__ __forceinline__ void vgap(f32x16& s, f32x16& dp, const f32x4 (&lq)[4], u32x4 (&pp)[2], u32x4 (&pd)[2],
+                                     float c) {
+  constexpr int n = (i + 1) * 64 / kVGaps - i * 64 / kVGaps;
+  vops_at<T, i>(s, dp, lq, pp, pd, c, std::make_integer_sequence<int, n>{});
+}
+
+}  // namespace kv128
+
+template <class T, bool kPooled>
+__global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const BwdParams p) {
+  using namespace bwd;
+  using namespace kv128;
+  using V8 = typename T::vec8;
+  constexpr int D = 128;
+  constexpr int KS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int RB = D * 2;
+  constexpr int fL = kPooled ? 2 : 0;   // stats fields of this branch: L' at fL, -Delta at fL + 1
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + kListOff);
+  int* list_n = reinterpret_cast<int*>(smem + kListOff + 2 * kMaxBlocks);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+
+  // ---- work item: bwd_dkdv_kernel's mapping (heavy text columns first, then XCD-contiguous) ----
+  const int BH = p.B * p.H;
+  const int nkb = kPooled ? p.nbkp : p.nbk;
+  const int split = kPooled ? (int)blockIdx.x % p.psplit : 0;
+  int bh, kblk;
+  if (kPooled) {
+    const int lin = (int)blockIdx.x / p.psplit;
+    bh = lin / nkb;
+    kblk = lin % nkb;
+  } else {
+    const int hr = min(p.heavy_rows, nkb);
+    const int n_heavy = hr * BH;
+    if ((int)blockIdx.x < n_heavy) {
+      kblk = nkb - 1 - (int)(blockIdx.x / BH);
+      bh = blockIdx.x % BH;
+    } else {
+      const int cols_left = nkb - hr;
+      const int lin = xcd_linear(blockIdx.x - n_heavy, cols_left * BH);
+      bh = lin / cols_left;
+      kblk = cols_left - 1 - lin % cols_left;
+    }
+  }
+  const int b = bh / p.H, h = bh % p.H;
+  int Lq = p.Lq, Lk = p.Lk;
+  int64_t qrow0 = 0, krow0 = 0;
+  if (p.cu_q) {
+    qrow0 = p.cu_q[b]; Lq = p.cu_q[b + 1] - p.cu_q[b];
+    krow0 = p.cu_k[b]; Lk = p.cu_k[b + 1] - p.cu_k[b];
+  }
+  const int Lkey = kPooled ? p.Lkp : Lk;
+  const int k0 = kblk * kBlk;
+  if (k0 >= Lkey || Lq <= 0) return;
+  const int nbq = (Lq + kBlk - 1) / kBlk;
+
+  bool nan_head = false;
+  const uint8_t* mcol = nullptr;
+  if (!kPooled) {
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head, p.hm_mode);
+    if (mh) mcol = mh + kblk;
+  }
+  const int qlo = kPooled ? split * nbq / p.psplit : 0;
+  const int qhi = kPooled ? (split + 1) * nbq / p.psplit : nbq;
+  if (threadIdx.x < 64) {   // the q-blocks that keep this key block
+    int n = 0;
+    for (int i0 = qlo; i0 < qhi; i0 += 64) {
+      const int i = i0 + lane;
+      const bool keep = (i < qhi) && (mcol == nullptr || mcol[(int64_t)i * p.ms[2]] != 0);
+      const unsigned long long bal = __ballot(keep);
+      if (keep) {
+        const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+        list[pos] = (uint16_t)i;
+      }
+      n += __popcll(bal);
+    }
+    if (lane == 0) *list_n = n;
+  }
+
+  // this wave's 32 keys as B operands (lane = key, d = 16 ks + 8 half + 0..7), held in AGPRs
+  const int key = k0 + wave * 32 + l32;
+  const bool kvalid = key < Lkey;
+  const int keyc = kvalid ? key : Lkey - 1;
+  const uint8_t* kb = kPooled
+      ? reinterpret_cast<const uint8_t*>(p.kp) + 2 * (b * p.kps[0] + h * p.kps[1] + (int64_t)keyc * p.kps[2])
+      : reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + (krow0 + keyc) * p.ks[2]);
+  const uint8_t* vb_ = kPooled
+      ? reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1] + (int64_t)keyc * p.vps[2])
+      : reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + (krow0 + keyc) * p.vs[2]);
+  V8 kf[KS], vf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = *reinterpret_cast<const V8*>(kb + (16 * s + 8 * half) * 2);
+    vf[s] = *reinterpret_cast<const V8*>(vb_ + (16 * s + 8 * half) * 2);
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    to_agpr(kf[s]);
+    to_agpr(vf[s]);
+  }
+  __syncthreads();
+  const int nlist = __builtin_amdgcn_readfirstlane(*list_n);
+  int ntiles = 2 * nlist;
+  if (nlist > 0 && list[nlist - 1] == nbq - 1 && (nbq - 1) * kBlk + kT >= Lq) ntiles -= 1;
+
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[i][r] = dv[i][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < DT; ++i) {
+    to_agpr(dk[i]);
+    to_agpr(dv[i]);
+  }
+
+  if (ntiles > 0) {
+    const uint8_t* qsrc = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + qrow0 * p.qs[2]);
+    const uint8_t* dosrc = reinterpret_cast<const uint8_t*>(p.dout) + 2 * (b * p.dos[0] + h * p.dos[1] + qrow0 * p.dos[2]);
+    const int qrowb = 2 * (int)p.qs[2], dorowb = 2 * (int)p.dos[2];   // host: every slice < 2 GiB
+    const float* stsrc = p.stats + (int64_t)bh * p.ntile * 256;
+    const int qbytes = (int)((int64_t)(Lq - 1) * qrowb + RB);
+    const int dobytes = (int)((int64_t)(Lq - 1) * dorowb + RB);
+    const int stbytes = p.ntile * 1024;
+
+    // Tile tt -> ring slot tt % 4: piece k of this wave is Q rows 4(wave + 4k).. (k < 4), dO rows
+    // 4(wave + 4(k-4)).. (k < 8), and the stats KiB (wave 0) or a zero-extent piece into the sink
+    // (waves 1-3), so every wave issues kPieces per tile and every vmcnt is a constant. Tiles past
+    // the last one are zero-extent too (they land in slots nobody reads).
+    int voff[kPieces];
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) {
+      voff[k] = lane * 16;
+      if (k < 8) {
+        const int r = (wave + 4 * (k & 3)) * 4 + lane / 16;
+        const int c = (lane & 15) ^ dual_swz<D>(r);
+        voff[k] = r * (k < 4 ? qrowb : dorowb) + c * 16;
+      }
+    }
+    struct TileDma {
+      srd_t q, dout, st;
+      int soff_q, soff_do, soff_st;
+    };
+    auto tile_dma = [&](int tt, int qb) __attribute__((always_inline)) -> TileDma {
+      const bool live = tt < ntiles;
+      const int row0 = qb * kBlk + (tt & 1) * kT;
+      TileDma d;
+      d.q = srd_t{qsrc, live ? qbytes : 0};
+      d.dout = srd_t{dosrc, live ? dobytes : 0};
+      d.st = srd_t{stsrc, (live && wave == 0) ? stbytes : 0};
+      d.soff_q = row0 * qrowb;
+      d.soff_do = row0 * dorowb;
+      d.soff_st = (row0 / 64) * 1024;
+      return d;
+    };
+    auto piece = [&](const TileDma& d, int slot, int k) __attribute__((always_inline)) {
+      if (k < 4) dma16(d.q, smem + kQOff + slot * 16384 + (wave + 4 * k) * 1024, voff[k], d.soff_q);
+      else if (k < 8) dma16(d.dout, smem + kDOOff + slot * 16384 + (wave + 4 * (k - 4)) * 1024, voff[k], d.soff_do);
+      else dma16(d.st, smem + (wave == 0 ? kStOff + slot * 1024 : kSinkOff), voff[k], d.soff_st);
+    };
+    auto list_at = [&](int tt) __attribute__((always_inline)) -> int {
+      return __builtin_amdgcn_readfirstlane((int)list[min(tt >> 1, nlist - 1)]);
+    };
+
+    // lane addresses of the asm reads (slot, row-half and k-step offsets are immediates)
+    const uint32_t sbase = static_cast<uint32_t>(
+        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)smem));
+    uint32_t xa[2][KS];        // [Q, dO][ks]: row l32, chunk 2 ks + half
+    uint32_t ya[2][DT][2];     // [Q, dO][dt][+0, +8 rows]: transposed reads
+    const int trr = tr_row(lane), trc = tr_col(lane);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const uint32_t rb = sbase + (m ? kDOOff : kQOff);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xa[m][ks] = rb + l32 * RB + 16 * ((2 * ks + half) ^ dual_swz<D>(l32));
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int p8 = 0; p8 < 2; ++p8) {
+          const int r = trr + 8 * p8;
+          ya[m][dt][p8] = rb + r * RB + 16 * ((4 * dt + (trc >> 3)) ^ dual_swz<D>(r)) + 2 * (trc & 7);
+        }
+    }
+    const uint32_t sta = sbase + kStOff + 16 * half;
+    const uint32_t lista = sbase + kListOff;
+    const float c = p.c;
+
+    f32x16 s0, dp0, s1, dp1;     // scores / dP of rows 0-31 and 32-63
+    f32x4 dq0[4], dq1[4];        // -Delta seeds of dp0 / dp1 (asm reads)
+    f32x4 lq0[4], lq1[4];        // L' of rows 0-31 / 32-63 (asm reads)
+    u32x4 pp0[2], pd0[2], pp1[2], pd1[2];
+    V8 nx[kLA];                  // operands of the next tile's first kLA MFMAs (read in gaps 53-56)
+    uint32_t qb_raw = 0;         // the q-block of tile t+3 (asm read)
+    TileDma dn{};                // the DMA of tile t+3
+
+    // ---- prologue: tiles 0-2 in flight, tile 0 landed, its seeds and first operands read -------
+    dn = tile_dma(0, list_at(0));
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) piece(dn, 0, k);
+    dn = tile_dma(1, list_at(1));
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) piece(dn, 1, k);
+    dn = tile_dma(2, list_at(2));
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) piece(dn, 2, k);
+    VB_WAIT_VMCNT(2 * kPieces);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    rd128<(fL + 1) * 256 + 0 * 32>(dq0[0], sta);
+    rd128<(fL + 1) * 256 + 1 * 32>(dq0[1], sta);
+    rd128<(fL + 1) * 256 + 2 * 32>(dq0[2], sta);
+    rd128<(fL + 1) * 256 + 3 * 32>(dq0[3], sta);
+    rd128<0>(nx[0], xa[0][0]);
+    rd128<0>(nx[1], xa[1][0]);
+    if constexpr (kLA > 2) rd128<0>(nx[2], xa[0][1]);
+    if constexpr (kLA > 3) rd128<0>(nx[3], xa[1][1]);
+#if __HIP_DEVICE_COMPILE__
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+#pragma unroll
+    for (int j = 0; j < 4; ++j) launder(dq0[j]);
+#pragma unroll
+    for (int q = 0; q < kLA; ++q) launder(nx[q]);
+
+    // ---- one tile: U = slot of tile t, M = 0 steady, 1 first tile (no B section), 2 drain (only
+    // the B section of the last tile, gaps 0-31) ------------------------------------------------
+    auto iter = [&](int t, auto U, auto M) __attribute__((always_inline)) {
+      constexpr int u = decltype(U)::value;
+      constexpr int up = (u + 3) & 3, un = (u + 1) & 3;
+      constexpr int mode = decltype(M)::value;
+      V8 xop[64];
+      s16x4 ylo[64], yhi[64];
+      auto gap = [&](auto G) __attribute__((always_inline)) {
+        constexpr int g = decltype(G)::value;
+        constexpr int sc = g >> 4, i = g & 15;
+        // ---- MFMA g ----
+        if constexpr (sc == 0 || sc == 2) {
+          V8& a = g < kLA ? nx[g % kLA] : xop[g];
+          if constexpr (g >= kLA) wait1<wait_n(g)>(a);
+          if constexpr (g == 1 || g == 33) {
+            f32x4 (&dq)[4] = g == 1 ? dq0 : dq1;
+            f32x16& dp = g == 1 ? dp0 : dp1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              launder(dq[j]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) dp[4 * j + e] = dq[j][e];
+            }
+          }
+          if constexpr (mode != 2) {
+            f32x16& s = sc == 0 ? s0 : s1;
+            f32x16& dp = sc == 0 ? dp0 : dp1;
+            constexpr int ks = i >> 1;
+            if constexpr (i & 1) mf_vacc<T>(dp, a, vf[ks]);
+            else if constexpr (ks == 0) mf_zero<T>(s, a, kf[0]);
+            else mf_vacc<T>(s, a, kf[ks]);
+          }
+        } else {
+          wait2<wait_n(g)>(ylo[g], yhi[g]);
+          constexpr bool run = sc == 1 ? mode != 1 : mode != 2;
+          if constexpr (run) {
+            constexpr int j = i >> 1, sb = j >> 2, dt = j & 3;
+            const V8 a = join8<T>(ylo[g], yhi[g]);
+            if constexpr (i & 1) mf_aacc<T>(dk[dt], a, __builtin_bit_cast(V8, sc == 1 ? pd1[sb] : pd0[sb]));
+            else mf_aacc<T>(dv[dt], a, __builtin_bit_cast(V8, sc == 1 ? pp1[sb] : pp0[sb]));
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- fillers of gap g ----
+        constexpr int m = g + kLA;   // operand reads of MFMA m
+        if constexpr (m < 64) {
+          constexpr int ms = m >> 4, mi = m & 15;
+          if constexpr (ms == 0 || ms == 2) {
+            rd128<u * 16384 + (ms >> 1) * 8192>(xop[m], xa[mi & 1][mi >> 1]);
+          } else {
+            constexpr int slot = ms == 1 ? up : u;
+            constexpr int half_u = ms == 1 ? 1 : 0;
+            constexpr int j = mi >> 1, sb = j >> 2, dt = j & 3;
+            constexpr int mat = (mi & 1) ? 0 : 1;   // dK reads Q, dV reads dO
+            constexpr int imm = slot * 16384 + (32 * half_u + 16 * sb) * RB;
+            rdtr<imm>(ylo[m], ya[mat][dt][0]);
+            rdtr<imm>(yhi[m], ya[mat][dt][1]);
+          }
+        }
+        if constexpr (g == 8 || g == 9) {
+          constexpr int j = 2 * (g - 8);
+          rd128<u * 1024 + fL * 256 + (0 + 8 * j) * 4>(lq0[j], sta);
+          rd128<u * 1024 + fL * 256 + (0 + 8 * (j + 1)) * 4>(lq0[j + 1], sta);
+        }
+        if constexpr (g == 24 || g == 25) {
+          constexpr int j = 2 * (g - 24);
+          rd128<u * 1024 + (fL + 1) * 256 + (32 + 8 * j) * 4>(dq1[j], sta);
+          rd128<u * 1024 + (fL + 1) * 256 + (32 + 8 * (j + 1)) * 4>(dq1[j + 1], sta);
+        }
+        if constexpr (g == 40 || g == 41) {
+          constexpr int j = 2 * (g - 40);
+          rd128<u * 1024 + fL * 256 + (32 + 8 * j) * 4>(lq1[j], sta);
+          rd128<u * 1024 + fL * 256 + (32 + 8 * (j + 1)) * 4>(lq1[j + 1], sta);
+        }
+        if constexpr (g == 42) rdu16(qb_raw, lista + 2 * min((t + 3) >> 1, nlist - 1));
+        if constexpr (g == 53 || g == 54) {
+          constexpr int j = 2 * (g - 53);
+          rd128<un * 1024 + (fL + 1) * 256 + (8 * j) * 4>(dq0[j], sta);
+          rd128<un * 1024 + (fL + 1) * 256 + (8 * (j + 1)) * 4>(dq0[j + 1], sta);
+        }
+        if constexpr (g >= 53 && g < 53 + kLA) {
+          constexpr int q = g - 53;
+          rd128<un * 16384>(nx[q], xa[q & 1][q >> 1]);
+        }
+        // ---- score arithmetic ----
+        if constexpr (mode != 2 && g >= kV0 && g < kV0 + kVGaps) {
+          if constexpr (g == kV0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) launder(lq0[j]);
+          }
+          vgap<T, g - kV0>(s0, dp0, lq0, pp0, pd0, c);
+        }
+        if constexpr (mode != 2 && g >= kV1) {
+          if constexpr (g == kV1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) launder(lq1[j]);
+          }
+          vgap<T, g - kV1>(s1, dp1, lq1, pp1, pd1, c);
+        }
+        if constexpr (mode != 1 && g < kV1 + kVGaps - 64) vgap<T, g + 64 - kV1>(s1, dp1, lq1, pp1, pd1, c);
+        // ---- barrier and the DMA of tile t+3 into the slot tile t-1 left ----
+        if constexpr (mode != 2 && g == kV1) {
+          launder(qb_raw);
+          dn = tile_dma(t + 3, __builtin_amdgcn_readfirstlane((int)qb_raw));
+        }
+        if constexpr (mode != 2 && g == kGb) {
+          VB_WAIT_VMCNT(kPieces);   // tile t+1 landed (tile t+2 may be in flight)
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+        if constexpr (mode != 2 && g >= kGb && g < kGb + kPieces) piece(dn, up, g - kGb);
+        if constexpr (g == 63) {
+#pragma unroll
+          for (int q = 0; q < kLA; ++q) launder(nx[q]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      if constexpr (mode == 2) for_gaps(gap, std::make_integer_sequence<int, 32>{});
+      else for_gaps(gap, std::make_integer_sequence<int, 64>{});
+    };
+
+    // Tiles 1.. in groups of four (slots 1, 2, 3, 0: every LDS offset an immediate), so the loop
+    // body is one straight block; the up-to-three tiles past ntiles are zero tiles (zero-extent
+    // DMA: Q = dO = 0 and L' = -Delta = 0, hence P = 1, dP = 0, dS = 0: they add exact zeros).
+    iter(0, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    int t = 1;
+    for (; t < ntiles; t += 4) {
+      iter(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+      iter(t + 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{});
+      iter(t + 2, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{});
+      iter(t + 3, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    }
+    iter(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});   // B section of tile t-1
+#if __HIP_DEVICE_COMPILE__
+    // drain: the zero-extent DMA of tiles past the end must land before the LDS is released, and
+    // the dK/dV accumulators (asm MFMA results) need their wait states before the VALU reads them
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4"
+                 : "+a"(dk[0]), "+a"(dk[1]), "+a"(dk[2]), "+a"(dk[3]), "+a"(dv[0]), "+a"(dv[1]), "+a"(dv[2]),
+                   "+a"(dv[3])::"memory");
+#endif
+  }
+
+  // ---- epilogue: lane = key, registers = d (bwd_dkdv_kernel's) ---------------------------------
+  if (!kvalid) return;
+  const float nanf_ = __builtin_nanf("");
+  if (kPooled) {
+    const int64_t po = ((int64_t)split * BH + bh) * p.Lkp + key;
+    float* dkr = p.dkp_part + po * D;
+    float* dvr = p.dvp_part + po * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * half;
+        f32x4 a, cc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = dk[dt][4 * g4 + e] * p.scale;
+          cc[e] = dv[dt][4 * g4 + e];
+        }
+        *reinterpret_cast<f32x4*>(dkr + d) = a;
+        *reinterpret_cast<f32x4*>(dvr + d) = cc;
+      }
+    return;
+  }
+  // full-resolution key: + mean-pool adjoint of the pooled grads (replicate padding folds onto
+  // the last token), written at the caller's row
+  const float* pk = nullptr;
+  const float* pv = nullptr;
+  float pw = 0.f;
+  if (p.dkp) {
+    const int gp = key / p.gap;
+    pk = p.dkp + ((int64_t)bh * p.Lkp + gp) * D;
+    pv = p.dvp + ((int64_t)bh * p.Lkp + gp) * D;
+    const int extra = (key == Lk - 1) ? p.Lkp * p.gap - Lk : 0;
+    pw = (float)(1 + extra) / (float)p.gap;
+  }
+  const int64_t orow = p.kv_rows ? p.kv_rows[key] : krow0 + key;
+  uint8_t* dkr = reinterpret_cast<uint8_t*>(p.dk) + 2 * (b * p.dks[0] + h * p.dks[1] + orow * p.dks[2]);
+  uint8_t* dvr = reinterpret_cast<uint8_t*>(p.dv) + 2 * (b * p.dvs[0] + h * p.dvs[1] + orow * p.dvs[2]);
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * half;
+      float a[4], cc[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = dk[dt][4 * g4 + e] * p.scale;
+        cc[e] = dv[dt][4 * g4 + e];
+      }
+      if (pk) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(pk + d);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(pv + d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = fmaf(x[e], pw, a[e]);
+          cc[e] = fmaf(y[e], pw, cc[e]);
+        }
+      }
+      if (nan_head) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = cc[e] = nanf_;
+      }
+      u32x2 w, z;
+      w[0] = pack2<T>(a[0], a[1]); w[1] = pack2<T>(a[2], a[3]);
+      z[0] = pack2<T>(cc[0], cc[1]); z[1] = pack2<T>(cc[2], cc[3]);
+      *reinterpret_cast<u32x2*>(dkr + d * 2) = w;
+      *reinterpret_cast<u32x2*>(dvr + d * 2) = z;
+    }
+}
+
+bool dkdv128_enabled() {
+  const char* e = getenv("VB_BWD_KV128");
+  return e ? atoi(e) != 0 : VB_BWD_KV128_DEFAULT != 0;
+}
+
+int launch_dkdv128(const BwdParams& p, bool pooled, bool f16, hipStream_t s) {
+  const int BH = p.B * p.H;
+  if (pooled) {
+    const dim3 grid(p.nbkp * BH * p.psplit);
+    if (f16) hipLaunchKernelGGL((bwd_dkdv128_kernel<F16, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dkdv128_kernel<BF16, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    return check_launch("bwd_dkdv128_kernel<pooled>");
+  }
+  const dim3 grid(p.nbk * BH);
+  if (f16) hipLaunchKernelGGL((bwd_dkdv128_kernel<F16, false>), grid, dim3(bwd::kThreads), 0, s, p);
+  else hipLaunchKernelGGL((bwd_dkdv128_kernel<BF16, false>), grid, dim3(bwd::kThreads), 0, s, p);
+  return check_launch("bwd_dkdv128_kernel");
+}
+
+}  // namespace vb
