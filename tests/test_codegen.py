@@ -77,14 +77,14 @@ def test_makefile_falls_back_when_the_scheduler_option_is_gone():
     assert bad.returncode == 0 and "rejects" in bad.stderr and "no-such-option" not in bad.stdout
 
 
-# ---- the hand-scheduled D=128 dK/dV (vb_attn_bwd_kv128.hip) ---------------------------------------
+# ---- the hand-scheduled D=128 dK/dV (vb_attn_bwd_kv.hip) ---------------------------------------
 # Its LDS operands are read by inline asm and waited for with lgkmcnt counts derived from the
 # schedule, invisible to hipcc: a register spill or copy of an asm-read value before its wait, or a
 # miscounted wait, would read stale data. tools/diag/lgkm_check.py models the LDS counter over the
 # ISA and reports any such use.
-KV128_SRC = os.path.join(ROOT, "video-blade_amd", "csrc", "vb_attn_bwd_kv128.hip")
-KV128_KERNELS = [f"_ZN2vb18bwd_dkdv128_kernelINS_{t}ELb{p}EEEvNS_9BwdParamsE"
-                 for t in ("4BF16", "3F16") for p in (0, 1)]
+KV128_SRC = os.path.join(ROOT, "video-blade_amd", "csrc", "vb_attn_bwd_kv.hip")
+KV128_KERNELS = [f"_ZN2vb20bwd_dkdv_pipe_kernelILi{d}ENS_{t}ELb{p}EEEvNS_9BwdParamsE"
+                 for d in (64, 128) for t in ("4BF16", "3F16") for p in (0, 1)]
 
 
 @pytest.fixture(scope="module")

@@ -1015,11 +1015,11 @@ static int launch_prep(const PrepParams& pp, hipStream_t s) {
 template <int D, class T>
 static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
   const int BH = p.B * p.H;
-  const bool kv128 = D == 128 && dkdv128_enabled();
+  const bool pipe = dkdv_pipe_enabled(D);
   constexpr bool kF16 = std::is_same<T, F16>::value;
   if (pool && p.dkp) {
-    if (kv128) {
-      if (int rc = launch_dkdv128(p, true, kF16, s)) return rc;
+    if (pipe) {
+      if (int rc = launch_dkdv_pipe(p, D, true, kF16, s)) return rc;
     } else {
       hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true>), dim3(p.nbkp * BH * p.psplit), dim3(bwd::kThreads), 0, s, p);
       if (int rc = check_launch("bwd_dkdv_kernel<pooled>")) return rc;
@@ -1032,8 +1032,8 @@ static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
     }
   }
   if (p.k) {
-    if (kv128) {
-      if (int rc = launch_dkdv128(p, false, kF16, s)) return rc;
+    if (pipe) {
+      if (int rc = launch_dkdv_pipe(p, D, false, kF16, s)) return rc;
     } else {
       hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, false>), dim3(p.nbk * BH), dim3(bwd::kThreads), 0, s, p);
       if (int rc = check_launch("bwd_dkdv_kernel")) return rc;

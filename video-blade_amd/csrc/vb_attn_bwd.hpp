@@ -64,11 +64,11 @@ struct MlGeom {
   }
 };
 
-// The hand-scheduled D=128 dK/dV kernels (vb_attn_bwd_kv128.hip): returns 0 or a VB_ERR code.
-// `pooled` selects the pooled-key pass (grid nbkp * B*H * psplit) over the full-resolution one
-// (grid nbk * B*H).
-int launch_dkdv128(const BwdParams& p, bool pooled, bool f16, hipStream_t s);
-// VB_BWD_KV128 (env, default VB_BWD_KV128_DEFAULT): route D=128 dK/dV to those kernels
-bool dkdv128_enabled();
+// The hand-scheduled dK/dV kernels (vb_attn_bwd_kv.hip): returns 0 or a VB_ERR code. `pooled`
+// selects the pooled-key pass (grid nbkp * B*H * psplit) over the full-resolution one (grid nbk * B*H).
+int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream_t s);
+// env VB_BWD_KV128 / VB_BWD_KV64 (defaults VB_BWD_KV128_DEFAULT / VB_BWD_KV64_DEFAULT): route the
+// head dim's dK/dV to those kernels
+bool dkdv_pipe_enabled(int D);
 
 }  // namespace vb

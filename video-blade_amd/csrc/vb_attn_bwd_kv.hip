@@ -30,53 +30,86 @@
 #ifndef VB_BWD_KV128_DEFAULT
 #define VB_BWD_KV128_DEFAULT 1
 #endif
+#ifndef VB_KV64_WAVES
+#define VB_KV64_WAVES 1    // waves per SIMD the D=64 kernel is register-budgeted for (2 spills)
+#endif
+#ifndef VB_BWD_KV64_DEFAULT
+#define VB_BWD_KV64_DEFAULT 0
+#endif
 #ifndef VB_KV128_LA
 #define VB_KV128_LA 4      // operand lookahead in MFMAs
 #endif
+#ifndef VB_KV128_NODMA
+#define VB_KV128_NODMA 0   // diagnostic (wrong results): no DMA after the prologue
+#endif
+#ifndef VB_KV128_XNOP
+#define VB_KV128_XNOP 0    // 1: s_nop 1 ahead of the S/dP MFMAs too (measured 2 % slower on the Wan backward)
+#endif
+#if VB_KV128_XNOP
+#define KV_XNOP "s_nop 1\n\t"
+#else
+#define KV_XNOP ""
+#endif
 
 namespace vb {
-namespace kv128 {
+namespace kvp {
 
 constexpr int kLA = VB_KV128_LA;
-static_assert(kLA >= 2 && kLA <= 4, "lookahead out of range (the next tile's operands are read in gaps 53-56)");
-// LDS map (bytes): Q ring 4 x 16 KiB, dO ring 4 x 16 KiB, stats ring 4 x 1 KiB, the 1 KiB sink of
-// the waves' padding DMA piece, the q-block list
-constexpr int kQOff = 0;
-constexpr int kDOOff = 65536;
-constexpr int kStOff = 131072;
-constexpr int kSinkOff = kStOff + 4096;
-constexpr int kListOff = kSinkOff + 1024;
-constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16;
-constexpr int kPieces = 9;   // LDS-DMA pieces per wave and tile: 4 of Q, 4 of dO, stats (wave 0) or sink
-constexpr int kGb = 52;      // gap of the tile barrier; DMA pieces in gaps kGb .. kGb + 8
-constexpr int kV0 = 18;      // V(t,0): gaps 18..47
-constexpr int kV1 = 50;      // V(t,1): gaps 50..63, then 0..15 of the next tile
-constexpr int kVGaps = 30;
+static_assert(kLA >= 2 && kLA <= 4, "lookahead out of range (the next tile's operands are read in 4 gaps)");
 
-// ---- the LDS read schedule (drives both the issue and the lgkmcnt of every wait) ----------------
-// gap h issues, in order: the operand reads of MFMA h + kLA (X: one ds_read_b128; Y: two
-// ds_read_b64_tr_b16), unless h + kLA >= 64; then the extra reads of extra_reads(h):
-//   8, 9  L' of rows 0-31 (two f32x4 each)         24, 25  -Delta of rows 32-63 (dP seeds)
-//   40, 41 L' of rows 32-63                        42      the q-block of tile t+3 (list entry)
-//   53, 54 -Delta of tile t+1's rows 0-31 + the operand of its MFMA 0 / 1
-//   55, 56 the operands of tile t+1's MFMAs 2 / 3
-constexpr int op_reads(int g) { return ((g >> 4) & 1) ? 2 : 1; }
-constexpr int extra_reads(int h) {
-  return (h == 8 || h == 9 || h == 24 || h == 25 || h == 40 || h == 41) ? 2
-         : (h == 53 || h == 54) ? 2 + (h - 53 < kLA)
-         : (h == 55 || h == 56) ? (h - 53 < kLA)
-         : h == 42 ? 1 : 0;
-}
-constexpr int gap_reads(int h) { return (h + kLA < 64 ? op_reads(h + kLA) : 0) + extra_reads(h); }
-// lgkmcnt before MFMA g: the reads issued after g's operand (LDS returns in order); MFMAs
-// 0..kLA-1 read operands completed before the tile started
-constexpr int wait_n(int g) {
-  if (g < kLA) return 15;
-  int n = extra_reads(g - kLA);
-  for (int h = g - kLA + 1; h < g; ++h) n += gap_reads(h);
-  return n > 15 ? 15 : n;
-}
-static_assert(extra_reads(kGb) == 0 && extra_reads(kGb - 1) == 0, "no read beside the barrier");
+// The per-tile schedule of head dim D: kSec MFMAs per section, N = 4 kSec per tile (gaps 0..N-1).
+// LDS map (bytes): Q ring 4 x kTileBytes, dO ring 4 x kTileBytes, stats ring 4 x 1 KiB, the 1 KiB
+// sink of the waves' padding DMA piece, the q-block list.
+template <int D>
+struct Sched {
+  static constexpr int KS = D / 16, DT = D / 32, RB = 2 * D;
+  static constexpr int kTileBytes = bwd::kT * RB;
+  static constexpr int kSec = 2 * KS;        // 16 at D=128, 8 at D=64
+  static constexpr int N = 4 * kSec;
+  static constexpr int kQOff = 0;
+  static constexpr int kDOOff = 4 * kTileBytes;
+  static constexpr int kStOff = 8 * kTileBytes;
+  static constexpr int kSinkOff = kStOff + 4096;
+  static constexpr int kListOff = kSinkOff + 1024;
+  static constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16;
+  static constexpr int kPQ = kTileBytes / 1024 / 4;   // LDS-DMA pieces per wave and matrix
+  static constexpr int kPieces = 2 * kPQ + 1;          // + stats (wave 0) or sink
+  static constexpr int kRpp = 1024 / RB;               // rows per piece
+  // V(t,0) in gaps kV0 .. kV0 + kV0n - 1 (after X(t,0), before Y(t,0)); V(t,1) in gaps kV1 .. N-1
+  // and 0 .. kSec-1 of the next tile (before Y(t,1))
+  static constexpr int kV0 = kSec + 2, kV0n = 2 * kSec - 2;
+  static constexpr int kV1 = 3 * kSec + 2, kV1n = 2 * kSec - 2;
+  static constexpr int kGb = N - 12;                   // the tile barrier
+  static constexpr int kDma0 = kGb > kV1 ? kGb : kV1;  // DMA pieces of tile t+3 from here (needs the list entry)
+  static constexpr int kLq0 = kV0 - 10;                // L' of rows 0-31 (two gaps)
+  static constexpr int kDq1 = 2 * kSec - 8;            // -Delta seeds of rows 32-63 (two gaps)
+  static constexpr int kLq1 = 3 * kSec - 8;            // L' of rows 32-63 (two gaps)
+  static constexpr int kList = 3 * kSec - 6;           // the q-block of tile t+3
+  static constexpr int kNx = kGb + 1;                  // tile t+1: -Delta seeds (2 gaps) and first operands
+  static_assert(kDma0 + kPieces <= N, "DMA pieces past the tile");
+  static_assert(kNx + 3 <= N - 1 - kLA, "next tile's operands must be covered by the last MFMA's wait");
+
+  // ---- the LDS read schedule (drives both the issue and the lgkmcnt of every wait) ------------
+  // gap h issues, in order: the operand reads of MFMA h + kLA (X: one ds_read_b128; Y: two
+  // ds_read_b64_tr_b16), unless h + kLA >= N; then the extra reads of extra_reads(h)
+  static constexpr int op_reads(int g) { return ((g / kSec) & 1) ? 2 : 1; }
+  static constexpr int extra_reads(int h) {
+    return (h == kLq0 || h == kLq0 + 1 || h == kDq1 || h == kDq1 + 1 || h == kLq1 || h == kLq1 + 1) ? 2
+           : (h == kNx || h == kNx + 1) ? 2 + (h - kNx < kLA)
+           : (h == kNx + 2 || h == kNx + 3) ? (h - kNx < kLA)
+           : h == kList ? 1 : 0;
+  }
+  static constexpr int gap_reads(int h) { return (h + kLA < N ? op_reads(h + kLA) : 0) + extra_reads(h); }
+  // lgkmcnt before MFMA g: the reads issued after g's operand (LDS returns in order); MFMAs
+  // 0..kLA-1 read operands completed before the tile started
+  static constexpr int wait_n(int g) {
+    if (g < kLA) return 15;
+    int n = extra_reads(g - kLA);
+    for (int h = g - kLA + 1; h < g; ++h) n += gap_reads(h);
+    return n > 15 ? 15 : n;
+  }
+  static_assert(extra_reads(kGb) == 0 && extra_reads(kGb - 1) == 0, "no read beside the barrier");
+};
 
 template <class F, int... Gs>
 __device__ __forceinline__ void for_gaps(F&& f, std::integer_sequence<int, Gs...>) {
@@ -88,18 +121,26 @@ template <class T>
 __device__ __forceinline__ void mf_zero(f32x16& d, const typename T::vec8& a, const typename T::vec8& b) {
 #if __HIP_DEVICE_COMPILE__
   if constexpr (std::is_same<T, BF16>::value)
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
+    asm volatile(KV_XNOP "v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
   else
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
+    asm volatile(KV_XNOP "v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
 #endif
 }
-template <class T>
+// kSeed: the first MFMA of a dP chain, whose C operand (the -Delta seeds) may have been assembled by
+// VALU moves: always padded
+template <class T, bool kSeed = false>
 __device__ __forceinline__ void mf_vacc(f32x16& d, const typename T::vec8& a, const typename T::vec8& b) {
 #if __HIP_DEVICE_COMPILE__
-  if constexpr (std::is_same<T, BF16>::value)
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
-  else
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+  if constexpr (kSeed && !VB_KV128_XNOP) {
+    if constexpr (std::is_same<T, BF16>::value)
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+    else
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+  } else if constexpr (std::is_same<T, BF16>::value) {
+    asm volatile(KV_XNOP "v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+  } else {
+    asm volatile(KV_XNOP "v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+  }
 #endif
 }
 template <class T>
@@ -169,35 +210,34 @@ __device__ __forceinline__ void vop(f32x16& s, f32x16& dp, const f32x4 (&lq)[4],
   else if constexpr (r < 8) pp[r >> 2][r & 3] = pack2<T>(s[2 * r], s[2 * r + 1]);
   else pd[(r - 8) >> 2][(r - 8) & 3] = pack2<T>(dp[2 * (r - 8)], dp[2 * (r - 8) + 1]);
 }
-template <class T, int i, int... Ks>
+template <class T, int lo, int... Ks>
 __device__ __forceinline__ void vops_at(f32x16& s, f32x16& dp, const f32x4 (&lq)[4], u32x4 (&pp)[2],
                                         u32x4 (&pd)[2], float c, std::integer_sequence<int, Ks...>) {
-  constexpr int lo = i * 64 / kVGaps;
   (vop<T, lo + Ks>(s, dp, lq, pp, pd, c), ...);
 }
-// the ops of gap i (0..kVGaps-1) of a half's arithmetic
-template <class T, int i>
+// the ops of gap i (0..n-1) of a half's arithmetic spread over n gaps
+template <class T, int i, int n>
 __device__ __forceinline__ void vgap(f32x16& s, f32x16& dp, const f32x4 (&lq)[4], u32x4 (&pp)[2], u32x4 (&pd)[2],
                                      float c) {
-  constexpr int n = (i + 1) * 64 / kVGaps - i * 64 / kVGaps;
-  vops_at<T, i>(s, dp, lq, pp, pd, c, std::make_integer_sequence<int, n>{});
+  constexpr int lo = i * 64 / n, hi = (i + 1) * 64 / n;
+  vops_at<T, lo>(s, dp, lq, pp, pd, c, std::make_integer_sequence<int, hi - lo>{});
 }
 
-}  // namespace kv128
+}  // namespace kvp
 
-template <class T, bool kPooled>
-__global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const BwdParams p) {
+// D=128: one workgroup per CU (one wave per SIMD); D=64: VB_KV64_WAVES
+template <int D, class T, bool kPooled>
+__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) bwd_dkdv_pipe_kernel(const BwdParams p) {
   using namespace bwd;
-  using namespace kv128;
+  using namespace kvp;
+  using S = Sched<D>;
   using V8 = typename T::vec8;
-  constexpr int D = 128;
-  constexpr int KS = D / 16;
-  constexpr int DT = D / 32;
-  constexpr int RB = D * 2;
+  constexpr int KS = S::KS, DT = S::DT, RB = S::RB, N = S::N, kSec = S::kSec, TB = S::kTileBytes;
+  constexpr int kPieces = S::kPieces, kPQ = S::kPQ;
   constexpr int fL = kPooled ? 2 : 0;   // stats fields of this branch: L' at fL, -Delta at fL + 1
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
-  uint16_t* list = reinterpret_cast<uint16_t*>(smem + kListOff);
-  int* list_n = reinterpret_cast<int*>(smem + kListOff + 2 * kMaxBlocks);
+  __shared__ __attribute__((aligned(16))) uint8_t smem[S::kLdsBytes];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + S::kListOff);
+  int* list_n = reinterpret_cast<int*>(smem + S::kListOff + 2 * kMaxBlocks);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -298,6 +338,7 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
     to_agpr(dk[i]);
     to_agpr(dv[i]);
   }
+  static_assert(DT == 2 || DT == 4, "head dim 64 or 128");
 
   if (ntiles > 0) {
     const uint8_t* qsrc = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + qrow0 * p.qs[2]);
@@ -308,18 +349,18 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
     const int dobytes = (int)((int64_t)(Lq - 1) * dorowb + RB);
     const int stbytes = p.ntile * 1024;
 
-    // Tile tt -> ring slot tt % 4: piece k of this wave is Q rows 4(wave + 4k).. (k < 4), dO rows
-    // 4(wave + 4(k-4)).. (k < 8), and the stats KiB (wave 0) or a zero-extent piece into the sink
-    // (waves 1-3), so every wave issues kPieces per tile and every vmcnt is a constant. Tiles past
-    // the last one are zero-extent too (they land in slots nobody reads).
+    // Tile tt -> ring slot tt % 4: piece k of this wave is Q rows kRpp (wave + 4k).. (k < kPQ), dO
+    // rows kRpp (wave + 4(k-kPQ)).. (k < 2 kPQ), and the stats KiB (wave 0) or a zero-extent piece
+    // into the sink (waves 1-3), so every wave issues kPieces per tile and every vmcnt is a
+    // constant. Tiles past the last one are zero-extent too (they land in slots nobody reads).
     int voff[kPieces];
 #pragma unroll
     for (int k = 0; k < kPieces; ++k) {
       voff[k] = lane * 16;
-      if (k < 8) {
-        const int r = (wave + 4 * (k & 3)) * 4 + lane / 16;
-        const int c = (lane & 15) ^ dual_swz<D>(r);
-        voff[k] = r * (k < 4 ? qrowb : dorowb) + c * 16;
+      if (k < 2 * kPQ) {
+        const int r = (wave + 4 * (k % kPQ)) * S::kRpp + lane / (RB / 16);
+        const int c = (lane % (RB / 16)) ^ dual_swz<D>(r);
+        voff[k] = r * (k < kPQ ? qrowb : dorowb) + c * 16;
       }
     }
     struct TileDma {
@@ -327,7 +368,7 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
       int soff_q, soff_do, soff_st;
     };
     auto tile_dma = [&](int tt, int qb) __attribute__((always_inline)) -> TileDma {
-      const bool live = tt < ntiles;
+      const bool live = tt < ntiles && !(VB_KV128_NODMA && tt >= 3);
       const int row0 = qb * kBlk + (tt & 1) * kT;
       TileDma d;
       d.q = srd_t{qsrc, live ? qbytes : 0};
@@ -339,9 +380,10 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
       return d;
     };
     auto piece = [&](const TileDma& d, int slot, int k) __attribute__((always_inline)) {
-      if (k < 4) dma16(d.q, smem + kQOff + slot * 16384 + (wave + 4 * k) * 1024, voff[k], d.soff_q);
-      else if (k < 8) dma16(d.dout, smem + kDOOff + slot * 16384 + (wave + 4 * (k - 4)) * 1024, voff[k], d.soff_do);
-      else dma16(d.st, smem + (wave == 0 ? kStOff + slot * 1024 : kSinkOff), voff[k], d.soff_st);
+      if (k < kPQ) dma16(d.q, smem + S::kQOff + slot * TB + (wave + 4 * k) * 1024, voff[k], d.soff_q);
+      else if (k < 2 * kPQ)
+        dma16(d.dout, smem + S::kDOOff + slot * TB + (wave + 4 * (k - kPQ)) * 1024, voff[k], d.soff_do);
+      else dma16(d.st, smem + (wave == 0 ? S::kStOff + slot * 1024 : S::kSinkOff), voff[k], d.soff_st);
     };
     auto list_at = [&](int tt) __attribute__((always_inline)) -> int {
       return __builtin_amdgcn_readfirstlane((int)list[min(tt >> 1, nlist - 1)]);
@@ -350,12 +392,17 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
     // lane addresses of the asm reads (slot, row-half and k-step offsets are immediates)
     const uint32_t sbase = static_cast<uint32_t>(
         reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)smem));
-    uint32_t xa[2][KS];        // [Q, dO][ks]: row l32, chunk 2 ks + half
-    uint32_t ya[2][DT][2];     // [Q, dO][dt][+0, +8 rows]: transposed reads
+    // When every dO offset fits the 16-bit immediate beside the Q ring (D=64), the dO reads use the
+    // Q reads' address registers with +kDOOff in the immediate (NA = 1 address set, else 2).
+    constexpr bool kShare = S::kDOOff + 3 * TB + 48 * RB < 65536;
+    constexpr int NA = kShare ? 1 : 2;
+    constexpr int kDOImm = kShare ? S::kDOOff : 0;
+    uint32_t xa[NA][KS];       // [Q, dO][ks]: row l32, chunk 2 ks + half
+    uint32_t ya[NA][DT][2];    // [Q, dO][dt][+0, +8 rows]: transposed reads
     const int trr = tr_row(lane), trc = tr_col(lane);
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const uint32_t rb = sbase + (m ? kDOOff : kQOff);
+    for (int m = 0; m < NA; ++m) {
+      const uint32_t rb = sbase + (m ? S::kDOOff : S::kQOff);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) xa[m][ks] = rb + l32 * RB + 16 * ((2 * ks + half) ^ dual_swz<D>(l32));
 #pragma unroll
@@ -366,15 +413,15 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
           ya[m][dt][p8] = rb + r * RB + 16 * ((4 * dt + (trc >> 3)) ^ dual_swz<D>(r)) + 2 * (trc & 7);
         }
     }
-    const uint32_t sta = sbase + kStOff + 16 * half;
-    const uint32_t lista = sbase + kListOff;
+    const uint32_t sta = sbase + S::kStOff + 16 * half;
+    const uint32_t lista = sbase + S::kListOff;
     const float c = p.c;
 
     f32x16 s0, dp0, s1, dp1;     // scores / dP of rows 0-31 and 32-63
     f32x4 dq0[4], dq1[4];        // -Delta seeds of dp0 / dp1 (asm reads)
     f32x4 lq0[4], lq1[4];        // L' of rows 0-31 / 32-63 (asm reads)
     u32x4 pp0[2], pd0[2], pp1[2], pd1[2];
-    V8 nx[kLA];                  // operands of the next tile's first kLA MFMAs (read in gaps 53-56)
+    V8 nx[kLA];                  // operands of the next tile's first kLA MFMAs (read from gap kNx)
     uint32_t qb_raw = 0;         // the q-block of tile t+3 (asm read)
     TileDma dn{};                // the DMA of tile t+3
 
@@ -396,9 +443,9 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
     rd128<(fL + 1) * 256 + 2 * 32>(dq0[2], sta);
     rd128<(fL + 1) * 256 + 3 * 32>(dq0[3], sta);
     rd128<0>(nx[0], xa[0][0]);
-    rd128<0>(nx[1], xa[1][0]);
+    rd128<kDOImm>(nx[1], xa[NA - 1][0]);
     if constexpr (kLA > 2) rd128<0>(nx[2], xa[0][1]);
-    if constexpr (kLA > 3) rd128<0>(nx[3], xa[1][1]);
+    if constexpr (kLA > 3) rd128<kDOImm>(nx[3], xa[NA - 1][1]);
 #if __HIP_DEVICE_COMPILE__
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -413,16 +460,16 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
       constexpr int u = decltype(U)::value;
       constexpr int up = (u + 3) & 3, un = (u + 1) & 3;
       constexpr int mode = decltype(M)::value;
-      V8 xop[64];
-      s16x4 ylo[64], yhi[64];
+      V8 xop[N];
+      s16x4 ylo[N], yhi[N];
       auto gap = [&](auto G) __attribute__((always_inline)) {
         constexpr int g = decltype(G)::value;
-        constexpr int sc = g >> 4, i = g & 15;
+        constexpr int sc = g / kSec, i = g % kSec;
         // ---- MFMA g ----
         if constexpr (sc == 0 || sc == 2) {
           V8& a = g < kLA ? nx[g % kLA] : xop[g];
-          if constexpr (g >= kLA) wait1<wait_n(g)>(a);
-          if constexpr (g == 1 || g == 33) {
+          if constexpr (g >= kLA) wait1<S::wait_n(g)>(a);
+          if constexpr (g == 1 || g == 2 * kSec + 1) {
             f32x4 (&dq)[4] = g == 1 ? dq0 : dq1;
             f32x16& dp = g == 1 ? dp0 : dp1;
 #pragma unroll
@@ -436,15 +483,15 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
             f32x16& s = sc == 0 ? s0 : s1;
             f32x16& dp = sc == 0 ? dp0 : dp1;
             constexpr int ks = i >> 1;
-            if constexpr (i & 1) mf_vacc<T>(dp, a, vf[ks]);
+            if constexpr (i & 1) mf_vacc<T, i == 1>(dp, a, vf[ks]);
             else if constexpr (ks == 0) mf_zero<T>(s, a, kf[0]);
             else mf_vacc<T>(s, a, kf[ks]);
           }
         } else {
-          wait2<wait_n(g)>(ylo[g], yhi[g]);
+          wait2<S::wait_n(g)>(ylo[g], yhi[g]);
           constexpr bool run = sc == 1 ? mode != 1 : mode != 2;
           if constexpr (run) {
-            constexpr int j = i >> 1, sb = j >> 2, dt = j & 3;
+            constexpr int j = i >> 1, sb = j / DT, dt = j % DT;
             const V8 a = join8<T>(ylo[g], yhi[g]);
             if constexpr (i & 1) mf_aacc<T>(dk[dt], a, __builtin_bit_cast(V8, sc == 1 ? pd1[sb] : pd0[sb]));
             else mf_aacc<T>(dv[dt], a, __builtin_bit_cast(V8, sc == 1 ? pp1[sb] : pp0[sb]));
@@ -453,80 +500,99 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
         __builtin_amdgcn_sched_barrier(0);
         // ---- fillers of gap g ----
         constexpr int m = g + kLA;   // operand reads of MFMA m
-        if constexpr (m < 64) {
-          constexpr int ms = m >> 4, mi = m & 15;
+        if constexpr (m < N) {
+          constexpr int ms = m / kSec, mi = m % kSec;
           if constexpr (ms == 0 || ms == 2) {
-            rd128<u * 16384 + (ms >> 1) * 8192>(xop[m], xa[mi & 1][mi >> 1]);
+            rd128<u * TB + (ms >> 1) * 32 * RB + ((mi & 1) ? kDOImm : 0)>(xop[m], xa[(mi & 1) && !kShare][mi >> 1]);
           } else {
             constexpr int slot = ms == 1 ? up : u;
             constexpr int half_u = ms == 1 ? 1 : 0;
-            constexpr int j = mi >> 1, sb = j >> 2, dt = j & 3;
+            constexpr int j = mi >> 1, sb = j / DT, dt = j % DT;
             constexpr int mat = (mi & 1) ? 0 : 1;   // dK reads Q, dV reads dO
-            constexpr int imm = slot * 16384 + (32 * half_u + 16 * sb) * RB;
-            rdtr<imm>(ylo[m], ya[mat][dt][0]);
-            rdtr<imm>(yhi[m], ya[mat][dt][1]);
+            constexpr int imm = slot * TB + (32 * half_u + 16 * sb) * RB;
+            constexpr int imm2 = imm + (mat ? kDOImm : 0);
+            rdtr<imm2>(ylo[m], ya[mat && !kShare][dt][0]);
+            rdtr<imm2>(yhi[m], ya[mat && !kShare][dt][1]);
           }
         }
-        if constexpr (g == 8 || g == 9) {
-          constexpr int j = 2 * (g - 8);
+        if constexpr (g == S::kLq0 || g == S::kLq0 + 1) {
+          constexpr int j = 2 * (g - S::kLq0);
           rd128<u * 1024 + fL * 256 + (0 + 8 * j) * 4>(lq0[j], sta);
           rd128<u * 1024 + fL * 256 + (0 + 8 * (j + 1)) * 4>(lq0[j + 1], sta);
         }
-        if constexpr (g == 24 || g == 25) {
-          constexpr int j = 2 * (g - 24);
+        if constexpr (g == S::kDq1 || g == S::kDq1 + 1) {
+          constexpr int j = 2 * (g - S::kDq1);
           rd128<u * 1024 + (fL + 1) * 256 + (32 + 8 * j) * 4>(dq1[j], sta);
           rd128<u * 1024 + (fL + 1) * 256 + (32 + 8 * (j + 1)) * 4>(dq1[j + 1], sta);
         }
-        if constexpr (g == 40 || g == 41) {
-          constexpr int j = 2 * (g - 40);
+        if constexpr (g == S::kLq1 || g == S::kLq1 + 1) {
+          constexpr int j = 2 * (g - S::kLq1);
           rd128<u * 1024 + fL * 256 + (32 + 8 * j) * 4>(lq1[j], sta);
           rd128<u * 1024 + fL * 256 + (32 + 8 * (j + 1)) * 4>(lq1[j + 1], sta);
         }
-        if constexpr (g == 42) rdu16(qb_raw, lista + 2 * min((t + 3) >> 1, nlist - 1));
-        if constexpr (g == 53 || g == 54) {
-          constexpr int j = 2 * (g - 53);
+        if constexpr (g == S::kList) rdu16(qb_raw, lista + 2 * min((t + 3) >> 1, nlist - 1));
+        if constexpr (g == S::kNx || g == S::kNx + 1) {
+          constexpr int j = 2 * (g - S::kNx);
           rd128<un * 1024 + (fL + 1) * 256 + (8 * j) * 4>(dq0[j], sta);
           rd128<un * 1024 + (fL + 1) * 256 + (8 * (j + 1)) * 4>(dq0[j + 1], sta);
         }
-        if constexpr (g >= 53 && g < 53 + kLA) {
-          constexpr int q = g - 53;
-          rd128<un * 16384>(nx[q], xa[q & 1][q >> 1]);
+        if constexpr (g >= S::kNx && g < S::kNx + kLA) {
+          constexpr int q = g - S::kNx;
+          rd128<un * TB + ((q & 1) ? kDOImm : 0)>(nx[q], xa[(q & 1) && !kShare][q >> 1]);
         }
         // ---- score arithmetic ----
-        if constexpr (mode != 2 && g >= kV0 && g < kV0 + kVGaps) {
-          if constexpr (g == kV0) {
+        if constexpr (mode != 2 && g >= S::kV0 && g < S::kV0 + S::kV0n) {
+          if constexpr (g == S::kV0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) launder(lq0[j]);
           }
-          vgap<T, g - kV0>(s0, dp0, lq0, pp0, pd0, c);
+          vgap<T, g - S::kV0, S::kV0n>(s0, dp0, lq0, pp0, pd0, c);
         }
-        if constexpr (mode != 2 && g >= kV1) {
-          if constexpr (g == kV1) {
+        if constexpr (mode != 2 && g >= S::kV1) {
+          if constexpr (g == S::kV1) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) launder(lq1[j]);
           }
-          vgap<T, g - kV1>(s1, dp1, lq1, pp1, pd1, c);
+          vgap<T, g - S::kV1, S::kV1n>(s1, dp1, lq1, pp1, pd1, c);
         }
-        if constexpr (mode != 1 && g < kV1 + kVGaps - 64) vgap<T, g + 64 - kV1>(s1, dp1, lq1, pp1, pd1, c);
+        if constexpr (mode != 1 && g < S::kV1 + S::kV1n - N) vgap<T, g + N - S::kV1, S::kV1n>(s1, dp1, lq1, pp1, pd1, c);
         // ---- barrier and the DMA of tile t+3 into the slot tile t-1 left ----
-        if constexpr (mode != 2 && g == kV1) {
+        if constexpr (mode != 2 && g == S::kV1) {
           launder(qb_raw);
           dn = tile_dma(t + 3, __builtin_amdgcn_readfirstlane((int)qb_raw));
         }
-        if constexpr (mode != 2 && g == kGb) {
+        if constexpr (mode != 2 && g == S::kGb) {
           VB_WAIT_VMCNT(kPieces);   // tile t+1 landed (tile t+2 may be in flight)
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
         }
-        if constexpr (mode != 2 && g >= kGb && g < kGb + kPieces) piece(dn, up, g - kGb);
-        if constexpr (g == 63) {
+        if constexpr (mode != 2 && g >= S::kDma0 && g < S::kDma0 + kPieces) piece(dn, up, g - S::kDma0);
+        if constexpr (g == N - 1) {
 #pragma unroll
           for (int q = 0; q < kLA; ++q) launder(nx[q]);
         }
         __builtin_amdgcn_sched_barrier(0);
       };
-      if constexpr (mode == 2) for_gaps(gap, std::make_integer_sequence<int, 32>{});
-      else for_gaps(gap, std::make_integer_sequence<int, 64>{});
+      if constexpr (mode == 2) {
+        for_gaps(gap, std::make_integer_sequence<int, 2 * kSec>{});
+        // The drain stops after the B section with reads in flight whose consumers it never
+        // reaches (the L' of rows 0-31, the seeds of rows 32-63, the operands of the C section's
+        // first kLA MFMAs). Keep their
+        // registers live past a full wait: hipcc must not hand a register to another value while
+        // an LDS read is still due to write it.
+#if __HIP_DEVICE_COMPILE__
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          launder(lq0[j]);
+          launder(dq1[j]);
+        }
+#pragma unroll
+        for (int q = 2 * kSec; q < 2 * kSec + kLA; ++q) launder(xop[q]);
+      } else {
+        for_gaps(gap, std::make_integer_sequence<int, N>{});
+      }
     };
 
     // Tiles 1.. in groups of four (slots 1, 2, 3, 0: every LDS offset an immediate), so the loop
@@ -545,9 +611,8 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
     // drain: the zero-extent DMA of tiles past the end must land before the LDS is released, and
     // the dK/dV accumulators (asm MFMA results) need their wait states before the VALU reads them
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4"
-                 : "+a"(dk[0]), "+a"(dk[1]), "+a"(dk[2]), "+a"(dk[3]), "+a"(dv[0]), "+a"(dv[1]), "+a"(dv[2]),
-                   "+a"(dv[3])::"memory");
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+a"(dk[0]), "+a"(dk[1]), "+a"(dv[0]), "+a"(dv[1])::"memory");
+    if constexpr (DT == 4) asm volatile("s_nop 0" : "+a"(dk[2]), "+a"(dk[3]), "+a"(dv[2]), "+a"(dv[3])::"memory");
 #endif
   }
 
@@ -621,23 +686,28 @@ __global__ void __launch_bounds__(bwd::kThreads, 1) bwd_dkdv128_kernel(const Bwd
     }
 }
 
-bool dkdv128_enabled() {
-  const char* e = getenv("VB_BWD_KV128");
-  return e ? atoi(e) != 0 : VB_BWD_KV128_DEFAULT != 0;
+bool dkdv_pipe_enabled(int D) {
+  const char* e = getenv(D == 128 ? "VB_BWD_KV128" : "VB_BWD_KV64");
+  return e ? atoi(e) != 0 : (D == 128 ? VB_BWD_KV128_DEFAULT : VB_BWD_KV64_DEFAULT) != 0;
 }
 
-int launch_dkdv128(const BwdParams& p, bool pooled, bool f16, hipStream_t s) {
+template <int D>
+static int launch_pipe(const BwdParams& p, bool pooled, bool f16, hipStream_t s) {
   const int BH = p.B * p.H;
   if (pooled) {
     const dim3 grid(p.nbkp * BH * p.psplit);
-    if (f16) hipLaunchKernelGGL((bwd_dkdv128_kernel<F16, true>), grid, dim3(bwd::kThreads), 0, s, p);
-    else hipLaunchKernelGGL((bwd_dkdv128_kernel<BF16, true>), grid, dim3(bwd::kThreads), 0, s, p);
-    return check_launch("bwd_dkdv128_kernel<pooled>");
+    if (f16) hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<D, F16, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<D, BF16, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    return check_launch("bwd_dkdv_pipe_kernel<pooled>");
   }
   const dim3 grid(p.nbk * BH);
-  if (f16) hipLaunchKernelGGL((bwd_dkdv128_kernel<F16, false>), grid, dim3(bwd::kThreads), 0, s, p);
-  else hipLaunchKernelGGL((bwd_dkdv128_kernel<BF16, false>), grid, dim3(bwd::kThreads), 0, s, p);
-  return check_launch("bwd_dkdv128_kernel");
+  if (f16) hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<D, F16, false>), grid, dim3(bwd::kThreads), 0, s, p);
+  else hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<D, BF16, false>), grid, dim3(bwd::kThreads), 0, s, p);
+  return check_launch("bwd_dkdv_pipe_kernel");
+}
+
+int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream_t s) {
+  return D == 128 ? launch_pipe<128>(p, pooled, f16, s) : launch_pipe<64>(p, pooled, f16, s);
 }
 
 }  // namespace vb
