@@ -83,7 +83,7 @@ def test_makefile_falls_back_when_the_scheduler_option_is_gone():
 # miscounted wait, would read stale data. tools/diag/lgkm_check.py models the LDS counter over the
 # ISA and reports any such use.
 KV128_SRC = os.path.join(ROOT, "video-blade_amd", "csrc", "vb_attn_bwd_kv.hip")
-KV128_KERNELS = [f"_ZN2vb20bwd_dkdv_pipe_kernelILi{d}ENS_{t}ELb{p}EEEvNS_9BwdParamsE"
+KV128_KERNELS = [f"_ZN2vb{n}ILi{d}ENS_{t}ELb{p}EEEvNS_9BwdParamsE" for n in ("20bwd_dkdv_pipe_kernel", "18bwd_dq_pipe_kernel")
                  for d in (64, 128) for t in ("4BF16", "3F16") for p in (0, 1)]
 
 

@@ -1,10 +1,11 @@
-"""Static check of hand-counted LDS waits in a kernel's ISA (the asm reads of vb_attn_bwd_kv128.hip).
+"""Static check of hand-counted LDS waits in a kernel's ISA (the asm reads of vb_attn_bwd_kv.hip).
 
-Walks the kernel's instructions in text order and models the LDS counter: every ds_read* pushes its
-destination registers, every `s_waitcnt lgkmcnt(N)` retires the oldest reads until N remain (LDS
-returns in order). Any other instruction that names a register of a read still in flight -- as a
-source or a destination -- is reported. Text order follows the fall-through path, which for the
-kv128 kernel covers every transition the loop makes (prologue -> tile 0 -> steady tiles -> drain).
+Models the LDS counter over the kernel's control-flow graph: every ds_read* pushes its destination
+registers, every `s_waitcnt lgkmcnt(N)` retires the oldest reads until N remain (LDS returns in
+order). Any other instruction that names a register of a read still in flight -- as a source or a
+destination -- is reported. The walk follows every branch (`s_branch`, `s_cbranch_*`, fall-through)
+and visits each (block, in-flight state) pair once, so loops and the uniform branches hipcc emits
+for scalar selects are covered.
 
 Usage: python tools/diag/lgkm_check.py <file.s> <kernel symbol>
   (hipcc -O3 --offload-arch=gfx950 --cuda-device-only -S ... -o file.s)
@@ -13,6 +14,7 @@ import re
 import sys
 
 REG = re.compile(r"\b([va])\[(\d+):(\d+)\]|\b([va])(\d+)\b")
+LABEL = re.compile(r"^(\.?[A-Za-z_$][\w.$]*):")
 
 
 def regs(text):
@@ -22,56 +24,99 @@ def regs(text):
             out.update(f"{m.group(1)}{i}" for i in range(int(m.group(2)), int(m.group(3)) + 1))
         else:
             out.add(f"{m.group(4)}{m.group(5)}")
+    return frozenset(out)
+
+
+def blocks_of(lines, start, end):
+    """[(label, [(line_no, op, rest)], successors)] in text order."""
+    blocks, cur, label = [], [], "entry"
+    for ln in range(start + 1, end):
+        raw = lines[ln].split(";")[0].rstrip()
+        m = LABEL.match(raw.strip())
+        if m and not raw.startswith("\t"):
+            blocks.append([label, cur])
+            label, cur = m.group(1), []
+            continue
+        s = raw.strip()
+        if not s or s.startswith("."):
+            continue
+        op, _, rest = s.partition(" ")
+        cur.append((ln, op, rest.strip()))
+        if op.startswith("s_cbranch") or op == "s_branch" or op == "s_endpgm":
+            blocks.append([label, cur])    # a branch ends the block (hipcc marks the next one
+            label, cur = f"anon{ln}", []   # only with a "; %bb.N:" comment)
+    blocks.append([label, cur])
+    index = {b[0]: i for i, b in enumerate(blocks)}
+    out = []
+    for i, (label, ins) in enumerate(blocks):
+        succ = []
+        last = ins[-1] if ins else None
+        nxt = i + 1 if i + 1 < len(blocks) else None
+        if last and last[1] == "s_branch":
+            succ = [index[last[2]]]
+        elif last and last[1].startswith("s_cbranch"):
+            succ = [index[last[2]]] + ([nxt] if nxt is not None else [])
+        elif last and last[1] in ("s_endpgm", "s_setpc_b64"):
+            succ = []
+        elif nxt is not None:
+            succ = [nxt]
+        out.append((label, ins, succ))
     return out
 
 
-def check(path, name):
+def check(path, name, verbose=True):
     lines = open(path).read().split("\n")
     start = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
     end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
-    pending = []   # [(line, set of regs)]
-    errors = 0
-    n_reads = n_waits = 0
-    for ln in range(start + 1, end):
-        raw = lines[ln].split(";")[0].strip()
-        if not raw or raw.startswith(".") or raw.endswith(":"):
+    blocks = blocks_of(lines, start, end)
+    bad = {}
+    n_reads = sum(1 for _, ins, _ in blocks for _, op, _ in ins if op.startswith("ds_read"))
+    n_waits = sum(1 for _, ins, _ in blocks for _, op, r in ins if op == "s_waitcnt" and "lgkmcnt" in r)
+    seen = set()
+    work = [(0, ())]
+    while work:
+        bi, state = work.pop()
+        if (bi, state) in seen:
             continue
-        op, _, rest = raw.partition(" ")
-        if op.startswith("s_waitcnt"):
-            m = re.search(r"lgkmcnt\((\d+)\)", rest)
-            if m:
-                n_waits += 1
-                keep = int(m.group(1))
-                while len(pending) > keep:
-                    pending.pop(0)
-            continue
-        if op.startswith("ds_read"):
-            dst, _, src = rest.partition(",")
-            used = regs(src)
+        seen.add((bi, state))
+        pending = list(state)
+        _, ins, succ = blocks[bi]
+        for ln, op, rest in ins:
+            if op == "s_waitcnt":
+                m = re.search(r"lgkmcnt\((\d+)\)", rest)
+                if m:
+                    keep = int(m.group(1))
+                    while len(pending) > keep:
+                        pending.pop(0)
+                continue
+            if op.startswith("ds_read"):
+                dst, _, src = rest.partition(",")
+                used = regs(src)
+                for pl, pr in pending:
+                    if used & pr:
+                        bad.setdefault(ln, f"line {ln + 1}: address of {op} {rest!r} from read at line {pl + 1} in flight")
+                pending.append((ln, regs(dst)))
+                del pending[:-15]   # the 4-bit counter: the 16th outstanding read waits for the oldest
+                continue
+            if op.startswith("ds_"):
+                pending.append((ln, frozenset()))   # compiler-visible LDS op: counts, hipcc waits for it
+                del pending[:-15]
+                continue
+            if op.startswith("s_"):
+                continue
+            used = regs(rest)
             for pl, pr in pending:
-                if used & pr:
-                    print(f"line {ln + 1}: address of {raw!r} from read at line {pl + 1} still in flight")
-                    errors += 1
-            pending.append((ln, regs(dst)))
-            n_reads += 1
-            continue
-        if op.startswith("ds_"):
-            # compiler-visible LDS op: it also counts; the compiler waits for its own results
-            pending.append((ln, set()))
-            continue
-        if op.startswith("s_") and not op.startswith("s_load"):
-            continue
-        if op.startswith("s_load"):
-            pending = pending  # SMEM also counts in lgkm but returns out of order; the compiler
-            continue           # waits lgkmcnt(0) for it, which this model handles when it appears
-        used = regs(rest)
-        for pl, pr in pending:
-            hit = used & pr
-            if hit:
-                print(f"line {ln + 1}: {raw!r} uses {sorted(hit)[:4]} loaded at line {pl + 1}, not yet waited for")
-                errors += 1
-    print(f"{name}: {n_reads} LDS reads, {n_waits} lgkmcnt waits, {errors} violations")
-    return errors
+                hit = used & pr
+                if hit:
+                    bad.setdefault(ln, f"line {ln + 1}: {op} {rest!r} uses {sorted(hit)[:4]} loaded at line {pl + 1}, not yet waited for")
+        for s in succ:
+            work.append((s, tuple(pending)))
+    if verbose:
+        for ln in sorted(bad)[:20]:
+            print(bad[ln])
+        print(f"{name}: {n_reads} LDS reads, {n_waits} lgkmcnt waits, {len(blocks)} blocks, "
+              f"{len(seen)} block states, {len(bad)} violations")
+    return len(bad)
 
 
 if __name__ == "__main__":

@@ -1039,6 +1039,7 @@ static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
       if (int rc = check_launch("bwd_dkdv_kernel")) return rc;
     }
   }
+  if (dq_pipe_enabled(D)) return launch_dq_pipe(p, D, pool, kF16, s);
   if (pool)
     hipLaunchKernelGGL((bwd_dq_kernel<D, T, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
   else

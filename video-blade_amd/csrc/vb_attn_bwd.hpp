@@ -70,5 +70,8 @@ int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream
 // env VB_BWD_KV128 / VB_BWD_KV64 (defaults VB_BWD_KV128_DEFAULT / VB_BWD_KV64_DEFAULT): route the
 // head dim's dK/dV to those kernels
 bool dkdv_pipe_enabled(int D);
+// the hand-scheduled dQ kernels (same file; grid nbq * B*H), env VB_BWD_DQ128 / VB_BWD_DQ64
+int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s);
+bool dq_pipe_enabled(int D);
 
 }  // namespace vb

@@ -33,6 +33,12 @@
 #ifndef VB_KV64_WAVES
 #define VB_KV64_WAVES 1    // waves per SIMD the D=64 kernel is register-budgeted for (2 spills)
 #endif
+#ifndef VB_BWD_DQ128_DEFAULT
+#define VB_BWD_DQ128_DEFAULT 0
+#endif
+#ifndef VB_BWD_DQ64_DEFAULT
+#define VB_BWD_DQ64_DEFAULT 0
+#endif
 #ifndef VB_BWD_KV64_DEFAULT
 #define VB_BWD_KV64_DEFAULT 0
 #endif
@@ -188,6 +194,21 @@ __device__ __forceinline__ void launder(V& a) {
   asm volatile("" : "+v"(a));
 #endif
 }
+// a value the optimizer cannot see through (see tile_dma in bwd_dq_pipe_kernel)
+template <class V>
+__device__ __forceinline__ V opaque(V a) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(a));
+#endif
+  return a;
+}
+__device__ __forceinline__ int uniform(int a) { return __builtin_amdgcn_readfirstlane(a); }
+__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
 template <class V>
 __device__ __forceinline__ void to_agpr(V& a) {
 #if __HIP_DEVICE_COMPILE__
@@ -221,6 +242,78 @@ __device__ __forceinline__ void vgap(f32x16& s, f32x16& dp, const f32x4 (&lq)[4]
                                      float c) {
   constexpr int lo = i * 64 / n, hi = (i + 1) * 64 / n;
   vops_at<T, lo>(s, dp, lq, pp, pd, c, std::make_integer_sequence<int, hi - lo>{});
+}
+
+// ---- the dQ kernel's schedule (bwd_dq_pipe_kernel): per 64-key tile t, sections
+//   A = X(t,0) S^T = K.Q^T, dP^T = V.dO^T of keys 0-31 (kX MFMAs)   B = Y(t-1,1) dQ^T of keys 32-63 (kY)
+//   C = X(t,1) keys 32-63                                          D = Y(t,0)   keys 0-31
+template <int D>
+struct QSched {
+  static constexpr int KS = D / 16, DT = D / 32, RB = 2 * D;
+  static constexpr int kTileBytes = bwd::kT * RB;
+  static constexpr int kX = 2 * KS, kY = 2 * DT;
+  static constexpr int N = 2 * kX + 2 * kY;
+  static constexpr int kB = kX, kC = kX + kY, kD = 2 * kX + kY;
+  static constexpr int kKOff = 0;
+  static constexpr int kVOff = 4 * kTileBytes;
+  static constexpr int kListOff = 8 * kTileBytes;
+  static constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16;
+  static constexpr int kPQ = kTileBytes / 1024 / 4;
+  static constexpr int kPieces = 2 * kPQ;
+  static constexpr int kRpp = 1024 / RB;
+  static constexpr int kV0 = kB + 2, kV0n = kD - kV0;          // V(t,0): [kB+2, kD)
+  static constexpr int kV1 = kD + 2, kV1n = N - kV1 + kB;      // V(t,1): [kD+2, N) and [0, kB) of t+1
+  static constexpr int kGb = N - 12;                           // the tile barrier (after section B)
+  static constexpr int kList = kGb - 6;                        // the key block of tile t+3
+  static constexpr int kNx = kGb + 1;                          // tile t+1's first operands
+  static constexpr int kDma0 = kGb + 1;
+  static_assert(kGb >= kC, "the barrier must follow the reads of the previous tile");
+  static_assert(kDma0 + kPieces <= N, "DMA pieces past the tile");
+  static_assert(kNx + kLA - 1 <= N - 1 - kLA, "next tile's operands must be covered by the last MFMA's wait");
+  static constexpr int sec(int g) { return g < kB ? 0 : g < kC ? 1 : g < kD ? 2 : 3; }
+  static constexpr int sec0(int c) { return c == 0 ? 0 : c == 1 ? kB : c == 2 ? kC : kD; }
+  static constexpr int op_reads(int g) { return (sec(g) & 1) ? 2 : 1; }
+  static constexpr int extra_reads(int h) { return (h == kList || (h >= kNx && h < kNx + kLA)) ? 1 : 0; }
+  static constexpr int gap_reads(int h) { return (h + kLA < N ? op_reads(h + kLA) : 0) + extra_reads(h); }
+  static constexpr int wait_n(int g) {
+    if (g < kLA) return 15;
+    int n = extra_reads(g - kLA);
+    for (int h = g - kLA + 1; h < g; ++h) n += gap_reads(h);
+    return n > 15 ? 15 : n;
+  }
+  static_assert(extra_reads(kGb) == 0, "no read beside the barrier");
+};
+
+// d = a . b(AGPR) + c (c a separate VGPR tile: the dP^T chain's -Delta seeds)
+template <class T>
+__device__ __forceinline__ void mf_cacc(f32x16& d, const typename T::vec8& a, const typename T::vec8& b,
+                                        const f32x16& c) {
+#if __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same<T, BF16>::value)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(d) : "v"(a), "a"(b), "v"(c));
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %3" : "=&v"(d) : "v"(a), "a"(b), "v"(c));
+#endif
+}
+// op k (0..55) of one 32-key half of the dQ pass: P = exp2(S c + nL), dS = P * dP (dP seeded with
+// -Delta), pd = bf16 pairs of dS (the B operand of dQ^T += K^T.dS^T)
+template <class T, int k>
+__device__ __forceinline__ void qop(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl) {
+  constexpr int st = k >> 4, r = k & 15;
+  if constexpr (st == 0) s[r] = fmaf(s[r], c, nl);
+  else if constexpr (st == 1) s[r] = exp2_fast(s[r]);
+  else if constexpr (st == 2) dp[r] = dp[r] * s[r];
+  else pd[r >> 2][r & 3] = pack2<T>(dp[2 * r], dp[2 * r + 1]);
+}
+template <class T, int lo, int... Ks>
+__device__ __forceinline__ void qops_at(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl,
+                                        std::integer_sequence<int, Ks...>) {
+  (qop<T, lo + Ks>(s, dp, pd, c, nl), ...);
+}
+template <class T, int i, int n>
+__device__ __forceinline__ void qgap(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl) {
+  constexpr int lo = i * 56 / n, hi = (i + 1) * 56 / n;
+  qops_at<T, lo>(s, dp, pd, c, nl, std::make_integer_sequence<int, hi - lo>{});
 }
 
 }  // namespace kvp
@@ -686,6 +779,356 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// dQ: one workgroup per (b, h, 128-row q-block), wave = 32 query rows (bwd_dq_kernel's geometry and
+// math), kept full-resolution K/V tiles then the pooled ones, on the same hand-placed stream as the
+// dK/dV kernel above (QSched). Keys past a tile's end read as zero rows (buffer extent), which add
+// nothing to dQ (dQ^T += K^T.dS^T with K = 0).
+// ------------------------------------------------------------------------------------------------
+template <int D, class T, bool kPool>
+__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) bwd_dq_pipe_kernel(const BwdParams p) {
+  using namespace bwd;
+  using namespace kvp;
+  using S = QSched<D>;
+  using V8 = typename T::vec8;
+  constexpr int KS = S::KS, DT = S::DT, RB = S::RB, N = S::N, TB = S::kTileBytes;
+  constexpr int kPieces = S::kPieces, kPQ = S::kPQ;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[S::kLdsBytes];
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + S::kListOff);
+  int* list_n = reinterpret_cast<int*>(smem + S::kListOff + 2 * kMaxBlocks);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+
+  // heavy-first, then XCD-contiguous head-major (bwd_dq_kernel's mapping)
+  const int BH = p.B * p.H;
+  const int hr = min(p.heavy_rows, p.nbq);
+  const int n_heavy = hr * BH;
+  int qblk, bh;
+  if ((int)blockIdx.x < n_heavy) {
+    qblk = p.nbq - 1 - (int)(blockIdx.x / BH);
+    bh = blockIdx.x % BH;
+  } else {
+    const int rows_left = p.nbq - hr;
+    const int lin = xcd_linear(blockIdx.x - n_heavy, rows_left * BH);
+    bh = lin / rows_left;
+    qblk = rows_left - 1 - lin % rows_left;
+  }
+  const int b = bh / p.H, h = bh % p.H;
+  int Lq = p.Lq, Lk = p.Lk;
+  int64_t qrow0 = 0, krow0 = 0;
+  if (p.cu_q) {
+    qrow0 = p.cu_q[b]; Lq = p.cu_q[b + 1] - p.cu_q[b];
+    krow0 = p.cu_k[b]; Lk = p.cu_k[b + 1] - p.cu_k[b];
+  }
+  const int q0 = qblk * kBlk;
+  if (q0 >= Lq) return;
+  const int nbk = (Lk + kBlk - 1) / kBlk;
+
+  bool nan_head = false;
+  const uint8_t* mrow = nullptr;
+  const bool use_main = p.k != nullptr;
+  if (use_main) {
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head, p.hm_mode);
+    if (mh) mrow = mh + (int64_t)qblk * p.ms[2];
+  }
+  if (threadIdx.x < 64) {
+    int n = 0;
+    if (use_main) {
+      for (int j0 = 0; j0 < nbk; j0 += 64) {
+        const int j = j0 + lane;
+        const bool keep = (j < nbk) && (mrow == nullptr || mrow[j] != 0);
+        const unsigned long long bal = __ballot(keep);
+        if (keep) {
+          const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+          list[pos] = (uint16_t)j;
+        }
+        n += __popcll(bal);
+      }
+    }
+    if (lane == 0) *list_n = n;
+  }
+
+  // this wave's 32 query rows: Q and dO as B operands (lane = query), held in AGPRs
+  const int g = q0 + wave * 32 + l32;
+  const bool qvalid = g < Lq;
+  const int gc = qvalid ? g : Lq - 1;
+  V8 qf[KS], df[KS];
+  {
+    const uint8_t* qp = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + (qrow0 + gc) * p.qs[2]);
+    const uint8_t* dp_ = reinterpret_cast<const uint8_t*>(p.dout) + 2 * (b * p.dos[0] + h * p.dos[1] + (qrow0 + gc) * p.dos[2]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf[s] = *reinterpret_cast<const V8*>(qp + (16 * s + 8 * half) * 2);
+      df[s] = *reinterpret_cast<const V8*>(dp_ + (16 * s + 8 * half) * 2);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      to_agpr(qf[s]);
+      to_agpr(df[s]);
+    }
+  }
+  const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
+  const float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];   // D1, D2 = -Delta
+
+  __syncthreads();
+  const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
+  int ntm = 2 * nkept;
+  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kBlk + kT >= Lk) ntm -= 1;
+  const int ntp = kPool ? (p.Lkp + kT - 1) / kT : 0;
+  const int ntiles = ntm + ntp;
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[i][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < DT; ++i) to_agpr(dq[i]);
+
+  if (ntiles > 0) {
+    const uint8_t* kbase = use_main ? reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + krow0 * p.ks[2]) : nullptr;
+    const uint8_t* vbase = use_main ? reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + krow0 * p.vs[2]) : nullptr;
+    const uint8_t* kpbase = kPool ? reinterpret_cast<const uint8_t*>(p.kp) + 2 * (b * p.kps[0] + h * p.kps[1]) : nullptr;
+    const uint8_t* vpbase = kPool ? reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1]) : nullptr;
+    const int krowb = 2 * (int)p.ks[2], vrowb = 2 * (int)p.vs[2];
+    const int kprowb = kPool ? 2 * (int)p.kps[2] : 0, vprowb = kPool ? 2 * (int)p.vps[2] : 0;
+    const int kbytes = use_main ? (int)((int64_t)(Lk - 1) * krowb + RB) : 0;
+    const int vbytes = use_main ? (int)((int64_t)(Lk - 1) * vrowb + RB) : 0;
+    const int kpbytes = kPool ? (int)((int64_t)(p.Lkp - 1) * kprowb + RB) : 0;
+    const int vpbytes = kPool ? (int)((int64_t)(p.Lkp - 1) * vprowb + RB) : 0;
+    // piece k of this wave: K rows kRpp (wave + 4k).. (k < kPQ), V rows kRpp (wave + 4(k-kPQ))..;
+    // the lane's voffset per key source (main / pooled row strides)
+    int voff_m[kPieces], voff_p[kPieces];
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) {
+      const bool isv = k >= kPQ;
+      const int r = (wave + 4 * (k % kPQ)) * S::kRpp + lane / (RB / 16);
+      const int c16 = 16 * ((lane % (RB / 16)) ^ dual_swz<D>(r));
+      voff_m[k] = r * (isv ? vrowb : krowb) + c16;
+      voff_p[k] = r * (isv ? vprowb : kprowb) + c16;
+    }
+    struct TileDma {
+      srd_t k, v;
+      int soff_k, soff_v;
+      bool pooled;
+    };
+    // tile tt's source: kept block list[tt/2] half tt%2, then pooled tiles; past the end zero-extent
+    // Every select below takes opaque operands (readfirstlane / an empty asm): hipcc otherwise turns
+    // a select between two loads of captured locals into a load through a selected address, which
+    // moves those locals to scratch.
+    auto tile_dma = [&](int tt, int blk) __attribute__((always_inline)) -> TileDma {
+      TileDma d;
+      d.pooled = kPool && tt >= ntm;
+      const bool live = tt < ntiles;
+      const int kstart = d.pooled ? (tt - ntm) * kT : blk * kBlk + (tt & 1) * kT;
+      d.k = srd_t{d.pooled ? uniform_ptr(kpbase) : uniform_ptr(kbase),
+                  live ? (d.pooled ? uniform(kpbytes) : uniform(kbytes)) : 0};
+      d.v = srd_t{d.pooled ? uniform_ptr(vpbase) : uniform_ptr(vbase),
+                  live ? (d.pooled ? uniform(vpbytes) : uniform(vbytes)) : 0};
+      d.soff_k = kstart * (d.pooled ? uniform(kprowb) : uniform(krowb));
+      d.soff_v = kstart * (d.pooled ? uniform(vprowb) : uniform(vrowb));
+      return d;
+    };
+    auto piece = [&](const TileDma& d, int slot, int k) __attribute__((always_inline)) {
+      const int vo = d.pooled ? opaque(voff_p[k]) : opaque(voff_m[k]);
+      if (k < kPQ) dma16(d.k, smem + S::kKOff + slot * TB + (wave + 4 * k) * 1024, vo, d.soff_k);
+      else dma16(d.v, smem + S::kVOff + slot * TB + (wave + 4 * (k - kPQ)) * 1024, vo, d.soff_v);
+    };
+    auto list_at = [&](int tt) __attribute__((always_inline)) -> int {
+      return __builtin_amdgcn_readfirstlane((int)list[max(min(tt >> 1, nkept - 1), 0)]);
+    };
+
+    const uint32_t sbase = static_cast<uint32_t>(
+        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)smem));
+    constexpr bool kShare = S::kVOff + 3 * TB + 48 * RB < 65536;
+    constexpr int NA = kShare ? 1 : 2;
+    constexpr int kVImm = kShare ? S::kVOff : 0;
+    uint32_t xa[NA][KS];       // [K, V][ks]: key row l32, chunk 2 ks + half
+    uint32_t ya[DT][2];        // K^T transposed reads [dt][+0, +8 rows]
+    const int trr = tr_row(lane), trc = tr_col(lane);
+#pragma unroll
+    for (int m = 0; m < NA; ++m) {
+      const uint32_t rb = sbase + (m ? S::kVOff : S::kKOff);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xa[m][ks] = rb + l32 * RB + 16 * ((2 * ks + half) ^ dual_swz<D>(l32));
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int p8 = 0; p8 < 2; ++p8) {
+        const int r = trr + 8 * p8;
+        ya[dt][p8] = sbase + S::kKOff + r * RB + 16 * ((4 * dt + (trc >> 3)) ^ dual_swz<D>(r)) + 2 * (trc & 7);
+      }
+    const uint32_t lista = sbase + S::kListOff;
+    const float c = p.c;
+
+    f32x16 s0, dp0, s1, dp1;   // S^T / dP^T of keys 0-31 and 32-63 (lane = query)
+    f32x16 cdt;                // -Delta seeds of the current tile's key source
+    float nl0 = 0.f, nl1 = 0.f;   // -L' of the tile whose V(t,0) / V(t,1) runs
+    u32x4 pd0[2], pd1[2];
+    V8 nx[kLA];
+    uint32_t blk_raw = 0;
+    TileDma dn{};
+    auto set_class = [&](bool pooled) __attribute__((always_inline)) {
+      const float dr = pooled ? opaque(D2) : opaque(D1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cdt[r] = dr;
+      nl0 = pooled ? -opaque(L2) : -opaque(L1);
+    };
+
+    // ---- prologue: tiles 0-2 in flight, tile 0 landed, its first operands read ---------------
+    dn = tile_dma(0, list_at(0));
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) piece(dn, 0, k);
+    dn = tile_dma(1, list_at(1));
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) piece(dn, 1, k);
+    dn = tile_dma(2, list_at(2));
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) piece(dn, 2, k);
+    VB_WAIT_VMCNT(2 * kPieces);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    rd128<0>(nx[0], xa[0][0]);
+    rd128<kVImm>(nx[1], xa[NA - 1][0]);
+    if constexpr (kLA > 2) rd128<0>(nx[2], xa[0][1]);
+    if constexpr (kLA > 3) rd128<kVImm>(nx[3], xa[NA - 1][1]);
+#if __HIP_DEVICE_COMPILE__
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+#pragma unroll
+    for (int q = 0; q < kLA; ++q) launder(nx[q]);
+    set_class(kPool && 0 >= ntm);
+
+    auto iter = [&](int t, auto U, auto M) __attribute__((always_inline)) {
+      constexpr int u = decltype(U)::value;
+      constexpr int up = (u + 3) & 3, un = (u + 1) & 3;
+      constexpr int mode = decltype(M)::value;
+      V8 xop[N];
+      s16x4 ylo[N], yhi[N];
+      auto gap = [&](auto G) __attribute__((always_inline)) {
+        constexpr int g = decltype(G)::value;
+        constexpr int sc = S::sec(g), i = g - S::sec0(S::sec(g));
+        // ---- MFMA g ----
+        if constexpr (sc == 0 || sc == 2) {
+          V8& a = g < kLA ? nx[g % kLA] : xop[g];
+          if constexpr (g >= kLA) wait1<S::wait_n(g)>(a);
+          if constexpr (mode != 2) {
+            f32x16& s_ = sc == 0 ? s0 : s1;
+            f32x16& dp = sc == 0 ? dp0 : dp1;
+            constexpr int ks = i >> 1;
+            if constexpr (i & 1) {
+              if constexpr (ks == 0) mf_cacc<T>(dp, a, df[0], cdt);
+              else mf_vacc<T>(dp, a, df[ks]);
+            } else {
+              if constexpr (ks == 0) mf_zero<T>(s_, a, qf[0]);
+              else mf_vacc<T>(s_, a, qf[ks]);
+            }
+          }
+        } else {
+          wait2<S::wait_n(g)>(ylo[g], yhi[g]);
+          constexpr bool run = sc == 1 ? mode != 1 : mode != 2;
+          if constexpr (run) {
+            constexpr int sb = i / DT, dt = i % DT;
+            const V8 a = join8<T>(ylo[g], yhi[g]);
+            mf_aacc<T>(dq[dt], a, __builtin_bit_cast(V8, sc == 1 ? pd1[sb] : pd0[sb]));
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- fillers of gap g ----
+        constexpr int m = g + kLA;
+        if constexpr (m < N) {
+          constexpr int ms = S::sec(m), mi = m - S::sec0(ms);
+          if constexpr (ms == 0 || ms == 2) {
+            constexpr int kt = ms >> 1;
+            rd128<u * TB + kt * 32 * RB + ((mi & 1) ? kVImm : 0)>(xop[m], xa[(mi & 1) && !kShare][mi >> 1]);
+          } else {
+            constexpr int slot = ms == 1 ? up : u;
+            constexpr int kt = ms == 1 ? 1 : 0;
+            constexpr int sb = mi / DT, dt = mi % DT;
+            constexpr int imm = slot * TB + (32 * kt + 16 * sb) * RB;
+            rdtr<imm>(ylo[m], ya[dt][0]);
+            rdtr<imm>(yhi[m], ya[dt][1]);
+          }
+        }
+        if constexpr (g == S::kList) rdu16(blk_raw, lista + 2 * max(min((t + 3) >> 1, nkept - 1), 0));
+        if constexpr (g >= S::kNx && g < S::kNx + kLA) {
+          constexpr int q = g - S::kNx;
+          rd128<un * TB + ((q & 1) ? kVImm : 0)>(nx[q], xa[(q & 1) && !kShare][q >> 1]);
+        }
+        // ---- score arithmetic ----
+        if constexpr (mode != 2 && g >= S::kV0 && g < S::kV0 + S::kV0n) qgap<T, g - S::kV0, S::kV0n>(s0, dp0, pd0, c, nl0);
+        if constexpr (mode != 2 && g >= S::kV1) {
+          if constexpr (g == S::kV1) nl1 = nl0;
+          qgap<T, g - S::kV1, S::kV1n>(s1, dp1, pd1, c, nl1);
+        }
+        if constexpr (mode != 1 && g < S::kV1 + S::kV1n - N) qgap<T, g + N - S::kV1, S::kV1n>(s1, dp1, pd1, c, nl1);
+        // ---- barrier and the DMA of tile t+3 into the slot tile t-1 left ----
+        if constexpr (mode != 2 && g == S::kGb) {
+          VB_WAIT_VMCNT(kPieces);   // tile t+1 landed (tile t+2 may be in flight)
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          launder(blk_raw);
+          dn = tile_dma(t + 3, __builtin_amdgcn_readfirstlane((int)blk_raw));
+        }
+        if constexpr (mode != 2 && g >= S::kDma0 && g < S::kDma0 + kPieces) piece(dn, up, g - S::kDma0);
+        if constexpr (g == N - 1) {
+#pragma unroll
+          for (int q = 0; q < kLA; ++q) launder(nx[q]);
+          if constexpr (mode != 2) set_class(kPool && t + 1 >= ntm);   // tile t+1's seeds and -L'
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      if constexpr (mode == 2) {
+        for_gaps(gap, std::make_integer_sequence<int, S::kC>{});
+#if __HIP_DEVICE_COMPILE__
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+#pragma unroll
+        for (int q = S::kC; q < S::kC + kLA; ++q) launder(xop[q]);
+        if constexpr (S::kList < S::kC) launder(blk_raw);   // D=64: the list read falls inside the drain
+      } else {
+        for_gaps(gap, std::make_integer_sequence<int, N>{});
+      }
+    };
+
+    iter(0, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    int t = 1;
+    for (; t < ntiles; t += 4) {
+      iter(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+      iter(t + 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{});
+      iter(t + 2, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{});
+      iter(t + 3, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    }
+    iter(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});   // B section of tile t-1
+#if __HIP_DEVICE_COMPILE__
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+a"(dq[0]), "+a"(dq[1])::"memory");
+    if constexpr (DT == 4) asm volatile("s_nop 0" : "+a"(dq[2]), "+a"(dq[3])::"memory");
+#endif
+  }
+
+  if (!qvalid) return;
+  const float mul = nan_head ? __builtin_nanf("") : p.scale;
+  const int64_t orow = p.q_rows ? p.q_rows[g] : qrow0 + g;
+  uint8_t* ob = reinterpret_cast<uint8_t*>(p.dq) + 2 * (b * p.dqs[0] + h * p.dqs[1] + orow * p.dqs[2]);
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * half;
+      u32x2 w;
+      w[0] = pack2<T>(dq[dt][4 * g4 + 0] * mul, dq[dt][4 * g4 + 1] * mul);
+      w[1] = pack2<T>(dq[dt][4 * g4 + 2] * mul, dq[dt][4 * g4 + 3] * mul);
+      *reinterpret_cast<u32x2*>(ob + d * 2) = w;
+    }
+}
+
 bool dkdv_pipe_enabled(int D) {
   const char* e = getenv(D == 128 ? "VB_BWD_KV128" : "VB_BWD_KV64");
   return e ? atoi(e) != 0 : (D == 128 ? VB_BWD_KV128_DEFAULT : VB_BWD_KV64_DEFAULT) != 0;
@@ -704,6 +1147,28 @@ static int launch_pipe(const BwdParams& p, bool pooled, bool f16, hipStream_t s)
   if (f16) hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<D, F16, false>), grid, dim3(bwd::kThreads), 0, s, p);
   else hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<D, BF16, false>), grid, dim3(bwd::kThreads), 0, s, p);
   return check_launch("bwd_dkdv_pipe_kernel");
+}
+
+bool dq_pipe_enabled(int D) {
+  const char* e = getenv(D == 128 ? "VB_BWD_DQ128" : "VB_BWD_DQ64");
+  return e ? atoi(e) != 0 : (D == 128 ? VB_BWD_DQ128_DEFAULT : VB_BWD_DQ64_DEFAULT) != 0;
+}
+
+template <int D>
+static int launch_dq(const BwdParams& p, bool pool, bool f16, hipStream_t s) {
+  const dim3 grid(p.nbq * p.B * p.H);
+  if (pool) {
+    if (f16) hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, F16, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, BF16, true>), grid, dim3(bwd::kThreads), 0, s, p);
+  } else {
+    if (f16) hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, F16, false>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, BF16, false>), grid, dim3(bwd::kThreads), 0, s, p);
+  }
+  return check_launch("bwd_dq_pipe_kernel");
+}
+
+int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s) {
+  return D == 128 ? launch_dq<128>(p, pool, f16, s) : launch_dq<64>(p, pool, f16, s);
 }
 
 int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream_t s) {
