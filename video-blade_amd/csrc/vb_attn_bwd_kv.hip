@@ -40,7 +40,7 @@
 #define VB_BWD_DQ64_DEFAULT 0
 #endif
 #ifndef VB_BWD_KV64_DEFAULT
-#define VB_BWD_KV64_DEFAULT 0
+#define VB_BWD_KV64_DEFAULT 1
 #endif
 #ifndef VB_KV128_LA
 #define VB_KV128_LA 4      // operand lookahead in MFMAs
