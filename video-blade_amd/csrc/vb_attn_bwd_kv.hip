@@ -48,6 +48,10 @@
 #ifndef VB_KV128_NODMA
 #define VB_KV128_NODMA 0   // diagnostic (wrong results): no DMA after the prologue
 #endif
+#ifndef VB_KV_ABL
+#define VB_KV_ABL 0        // diagnostic ablations of the dK/dV kernel (wrong results): bit 0 no score
+                           // VALU, bit 1 no operand LDS reads in the loop
+#endif
 #ifndef VB_KV128_XNOP
 #define VB_KV128_XNOP 0    // 1: s_nop 1 ahead of the S/dP MFMAs too (measured 2 % slower on the Wan backward)
 #endif
@@ -593,7 +597,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
         __builtin_amdgcn_sched_barrier(0);
         // ---- fillers of gap g ----
         constexpr int m = g + kLA;   // operand reads of MFMA m
-        if constexpr (m < N) {
+        if constexpr (m < N && !(VB_KV_ABL & 2)) {
           constexpr int ms = m / kSec, mi = m % kSec;
           if constexpr (ms == 0 || ms == 2) {
             rd128<u * TB + (ms >> 1) * 32 * RB + ((mi & 1) ? kDOImm : 0)>(xop[m], xa[(mi & 1) && !kShare][mi >> 1]);
@@ -634,21 +638,21 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
           rd128<un * TB + ((q & 1) ? kDOImm : 0)>(nx[q], xa[(q & 1) && !kShare][q >> 1]);
         }
         // ---- score arithmetic ----
-        if constexpr (mode != 2 && g >= S::kV0 && g < S::kV0 + S::kV0n) {
+        if constexpr (!(VB_KV_ABL & 1) && mode != 2 && g >= S::kV0 && g < S::kV0 + S::kV0n) {
           if constexpr (g == S::kV0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) launder(lq0[j]);
           }
           vgap<T, g - S::kV0, S::kV0n>(s0, dp0, lq0, pp0, pd0, c);
         }
-        if constexpr (mode != 2 && g >= S::kV1) {
+        if constexpr (!(VB_KV_ABL & 1) && mode != 2 && g >= S::kV1) {
           if constexpr (g == S::kV1) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) launder(lq1[j]);
           }
           vgap<T, g - S::kV1, S::kV1n>(s1, dp1, lq1, pp1, pd1, c);
         }
-        if constexpr (mode != 1 && g < S::kV1 + S::kV1n - N) vgap<T, g + N - S::kV1, S::kV1n>(s1, dp1, lq1, pp1, pd1, c);
+        if constexpr (!(VB_KV_ABL & 1) && mode != 1 && g < S::kV1 + S::kV1n - N) vgap<T, g + N - S::kV1, S::kV1n>(s1, dp1, lq1, pp1, pd1, c);
         // ---- barrier and the DMA of tile t+3 into the slot tile t-1 left ----
         if constexpr (mode != 2 && g == S::kV1) {
           launder(qb_raw);
