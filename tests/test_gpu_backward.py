@@ -47,7 +47,10 @@ def _ops():
                                                (256, 128, torch.bfloat16, 1.0),
                                                (517, 64, torch.float16, 0.3),
                                                (260, 128, torch.bfloat16, 0.6),
-                                               (1000, 64, torch.bfloat16, 0.25)])
+                                               (1000, 64, torch.bfloat16, 0.25),
+                                               (333, 128, torch.float16, 0.4),
+                                               (40, 128, torch.bfloat16, 1.0),    # one partial tile
+                                               (40, 64, torch.float16, 1.0)])
 def test_block_sparse_bwd_matches_oracle(L, D, dtype, density):
     B, H = 1, 2
     q, k, v, do = (_rand(B, H, L, D, dtype=dtype, seed=s) for s in range(4))
@@ -62,6 +65,53 @@ def test_block_sparse_bwd_matches_oracle(L, D, dtype, density):
     for name, g, r in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
         assert torch.isfinite(g).all(), name
         assert rel(g, r) <= TOL, (name, rel(g, r))
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_pipeline_dkdv_agrees_with_round3_kernel(D, monkeypatch):
+    """The hand-scheduled dK/dV kernels (vb_attn_bwd_kv.hip, default) against the round-3
+    bwd_dkdv_kernel (VB_BWD_KV64/128=0) on the same inputs: bit-identical at D=64 (the same -Delta
+    seeding and summation order), within bf16 rounding at D=128 (the pipeline seeds dP with -Delta,
+    the round-3 D=128 kernel added it after the chain). dQ is the same kernel in both runs."""
+    B, H, L = 1, 2, 700
+    q, k, v, do = (_rand(B, H, L, D, seed=20 + s) for s in range(4))
+    nb = (L + 127) // 128
+    mask = O.block_mask_from_density(B, H, nb, nb, 0.5, seed=3)
+    ops = _ops()
+    qd, kd, vd, dod, md = (t.to(DEV) for t in (q, k, v, do, mask))
+    out, lse = ops.attention_fwd(qd, kd, vd, block_mask=md, need_lse=True)
+    env = "VB_BWD_KV64" if D == 64 else "VB_BWD_KV128"
+    monkeypatch.setenv(env, "1")
+    new = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
+    monkeypatch.setenv(env, "0")
+    old = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
+    assert torch.equal(new[0], old[0])                      # dq
+    for a, b in zip(new[1:], old[1:]):
+        if D == 64:
+            assert torch.equal(a, b)
+        else:
+            assert rel(a.float().cpu(), b.float().cpu()) <= 5e-3
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_pipeline_dq_opt_in_matches_default(D, monkeypatch):
+    """The opt-in hand-scheduled dQ (VB_BWD_DQ64/128=1; measured slower) stays correct:
+    against the default dQ kernel on a ragged length with a partial last key tile."""
+    B, H, L = 1, 2, 517
+    q, k, v, do = (_rand(B, H, L, D, seed=30 + s) for s in range(4))
+    nb = (L + 127) // 128
+    mask = O.block_mask_from_density(B, H, nb, nb, 0.5, seed=4)
+    ops = _ops()
+    qd, kd, vd, dod, md = (t.to(DEV) for t in (q, k, v, do, mask))
+    out, lse = ops.attention_fwd(qd, kd, vd, block_mask=md, need_lse=True)
+    env = "VB_BWD_DQ64" if D == 64 else "VB_BWD_DQ128"
+    monkeypatch.setenv(env, "1")
+    new = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
+    monkeypatch.setenv(env, "0")
+    old = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
+    assert torch.isfinite(new[0]).all()
+    assert rel(new[0].float().cpu(), old[0].float().cpu()) <= 5e-3
+    assert torch.equal(new[1], old[1]) and torch.equal(new[2], old[2])
 
 
 def test_bwd_empty_rows_and_columns_and_determinism():
