@@ -114,3 +114,40 @@ def test_kv128_no_spills(kv128_asm, name):
     meta = text[i:i + 600]   # the fields follow .name in the kernel's metadata block
     assert re.search(r"\.vgpr_spill_count:\s+0\b", meta), "VGPR spills in " + name
     assert re.search(r"\.private_segment_fixed_size:\s+0\b", meta), "scratch in " + name
+
+
+@pytest.mark.parametrize("name", KV128_KERNELS)
+def test_kv128_no_valu_to_asm_mfma_hazard(kv128_asm, name, capsys):
+    """The pipeline kernels' asm MFMAs carry no s_nop: every VALU write of an MFMA source register
+    must sit >= 2 wait states before it on every path (tools/diag/mfma_hazard_check.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools", "diag"))
+    import mfma_hazard_check
+    assert mfma_hazard_check.check(kv128_asm, name) == 0, capsys.readouterr().out[-2000:]
+
+
+SYNTH = """k:
+\tds_read_b128 v[4:7], v1 offset:16
+\tv_mov_b32_e32 v9, 0
+\tv_mfma_f32_32x32x16_bf16 a[0:15], v[8:11], v[12:15], a[0:15]
+\ts_waitcnt lgkmcnt(0)
+\tv_add_f32_e32 v20, v4, v5
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+def test_checkers_detect_synthetic_violations(tmp_path, capsys):
+    """Both ISA checkers report what they exist for: a VALU write one instruction before an MFMA
+    that reads it, and a use of an LDS-read register with no wait (v[8:11] overlaps none of the
+    pending read's v[4:7]; the v_add after lgkmcnt(0) is fine)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools", "diag"))
+    import lgkm_check
+    import mfma_hazard_check
+    f = tmp_path / "k.s"
+    f.write_text(SYNTH)
+    assert mfma_hazard_check.check(str(f), "k") == 1
+    assert lgkm_check.check(str(f), "k") == 0
+    f.write_text(SYNTH.replace("v[8:11], v[12:15]", "v[4:7], v[12:15]"))
+    assert lgkm_check.check(str(f), "k") == 1

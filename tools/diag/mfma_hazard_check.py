@@ -1,0 +1,111 @@
+"""Static check of the VALU-write -> MFMA-read hazard for inline-asm MFMAs (vb_attn_bwd_kv.hip).
+
+hipcc pads the wait states a VALU write needs before an MFMA reads the same register (2 on gfx950)
+only for the MFMAs it generates; an MFMA written in inline asm is invisible to that pass. This tool
+walks the kernel's control-flow graph (tools/diag/lgkm_check.py's block parser) and, for every
+v_mfma, looks back over the instructions issued just before it (each instruction is one wait state,
+`s_nop N` is N+1) on every path; a VALU instruction (v_*, other than an MFMA) that writes one of the
+MFMA's source registers within WAIT_STATES is reported.
+
+Usage: python tools/diag/mfma_hazard_check.py <file.s> <kernel symbol>
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from lgkm_check import blocks_of, regs  # noqa: E402
+
+WAIT_STATES = 2
+
+
+def operands(rest):
+    out, depth, cur = [], 0, ""
+    for ch in rest:
+        if ch == "[":
+            depth += 1
+        elif ch == "]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def check(path, name, verbose=True):
+    lines = open(path).read().split("\n")
+    start = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    blocks = blocks_of(lines, start, end)
+    preds = {i: [] for i in range(len(blocks))}
+    for i, (_, _, succ) in enumerate(blocks):
+        for s in succ:
+            preds[s].append(i)
+
+    def tail(bi, need, seen):
+        """instructions (line, op, rest) of the paths into block bi, newest first, covering `need`
+        wait states; one list per path"""
+        if need <= 0 or bi in seen:
+            return [[]]
+        seen = seen | {bi}
+        ins = blocks[bi][1]
+        acc, w = [], 0
+        for item in reversed(ins):
+            acc.append(item)
+            w += (int(item[2]) + 1) if item[1] == "s_nop" and item[2].isdigit() else 1
+            if w >= need:
+                return [acc]
+        paths = []
+        for p in preds[bi] or [None]:
+            if p is None:
+                paths.append(acc)
+            else:
+                for t in tail(p, need - w, seen):
+                    paths.append(acc + t)
+        return paths
+
+    bad = {}
+    n_mfma = 0
+    for bi, (_, ins, _) in enumerate(blocks):
+        for k, (ln, op, rest) in enumerate(ins):
+            if not op.startswith("v_mfma"):
+                continue
+            n_mfma += 1
+            ops = operands(rest)
+            srcs = frozenset().union(*(regs(o) for o in ops[1:4]))
+            before = list(reversed(ins[:k]))
+            paths = []
+            w = 0
+            acc = []
+            for item in before:
+                acc.append(item)
+                w += (int(item[2]) + 1) if item[1] == "s_nop" and item[2].isdigit() else 1
+                if w >= WAIT_STATES:
+                    break
+            if w >= WAIT_STATES:
+                paths = [acc]
+            else:
+                paths = [acc + t for p in (preds[bi] or []) for t in tail(p, WAIT_STATES - w, frozenset())] or [acc]
+            for path in paths:
+                ws = 0
+                for pl, pop, prest in path:
+                    if ws >= WAIT_STATES:
+                        break
+                    if pop.startswith("v_") and not pop.startswith("v_mfma"):
+                        dst = regs(operands(prest)[0]) if prest else frozenset()
+                        if dst & srcs:
+                            bad.setdefault(ln, f"line {ln + 1}: {op} reads {sorted(dst & srcs)[:4]} written by "
+                                               f"{pop} at line {pl + 1}, {ws} wait states before")
+                    ws += (int(prest) + 1) if pop == "s_nop" and prest.isdigit() else 1
+    if verbose:
+        for ln in sorted(bad)[:20]:
+            print(bad[ln])
+        print(f"{name}: {n_mfma} MFMAs, {len(bad)} VALU->MFMA hazards")
+    return len(bad)
+
+
+if __name__ == "__main__":
+    sys.exit(1 if check(sys.argv[1], sys.argv[2]) else 0)

@@ -19,8 +19,8 @@
 // operand read issued kLA gaps ahead (asm reads, waited with exact lgkmcnt counts derived from
 // the schedule below); the tile's row statistics; the barrier (gap 52) and the nine LDS-DMA
 // pieces of tile t+3 (gaps 52-60) into a 4-slot ring. K and V (the B operands of X) and the dK/dV
-// accumulators live in AGPRs; all MFMAs are asm (v_mfma_f32_32x32x16), preceded by s_nop 1 for
-// the VALU-write -> MFMA-read wait states the compiler cannot see.
+// accumulators live in AGPRs; all MFMAs are asm (v_mfma_f32_32x32x16); the VALU-write -> MFMA-read
+// wait states the compiler cannot see for them are checked on the ISA (tools/diag/mfma_hazard_check.py).
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -50,7 +50,20 @@
 #endif
 #ifndef VB_KV_ABL
 #define VB_KV_ABL 0        // diagnostic ablations of the dK/dV kernel (wrong results): bit 0 no score
-                           // VALU, bit 1 no operand LDS reads in the loop
+                           // VALU, bit 1 no operand LDS reads in the loop, bit 2 no tile barrier,
+                           // bit 4 no DMA after the prologue
+#endif
+// s_nop 1 ahead of the asm MFMAs that read VALU-written registers (the packed P / dS, the -Delta
+// seeds): off by default — the schedule places every such write >= 2 instructions before its MFMA,
+// which tools/diag/mfma_hazard_check.py verifies on the ISA in tests/test_codegen.py (measured
+// 2.2 % on the Wan backward)
+#ifndef VB_KV_YNOP
+#define VB_KV_YNOP 0
+#endif
+#if VB_KV_YNOP
+#define KV_YNOP "s_nop 1\n\t"
+#else
+#define KV_YNOP ""
 #endif
 #ifndef VB_KV128_XNOP
 #define VB_KV128_XNOP 0    // 1: s_nop 1 ahead of the S/dP MFMAs too (measured 2 % slower on the Wan backward)
@@ -81,7 +94,7 @@ struct Sched {
   static constexpr int kStOff = 8 * kTileBytes;
   static constexpr int kSinkOff = kStOff + 4096;
   static constexpr int kListOff = kSinkOff + 1024;
-  static constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16;
+  static constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16 + 4 * (bwd::kMaxBlocks / 64);
   static constexpr int kPQ = kTileBytes / 1024 / 4;   // LDS-DMA pieces per wave and matrix
   static constexpr int kPieces = 2 * kPQ + 1;          // + stats (wave 0) or sink
   static constexpr int kRpp = 1024 / RB;               // rows per piece
@@ -143,9 +156,9 @@ __device__ __forceinline__ void mf_vacc(f32x16& d, const typename T::vec8& a, co
 #if __HIP_DEVICE_COMPILE__
   if constexpr (kSeed && !VB_KV128_XNOP) {
     if constexpr (std::is_same<T, BF16>::value)
-      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+      asm volatile(KV_YNOP "v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
     else
-      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
+      asm volatile(KV_YNOP "v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
   } else if constexpr (std::is_same<T, BF16>::value) {
     asm volatile(KV_XNOP "v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "a"(b));
   } else {
@@ -157,9 +170,9 @@ template <class T>
 __device__ __forceinline__ void mf_aacc(f32x16& d, const typename T::vec8& a, const typename T::vec8& b) {
 #if __HIP_DEVICE_COMPILE__
   if constexpr (std::is_same<T, BF16>::value)
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
+    asm volatile(KV_YNOP "v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
   else
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
+    asm volatile(KV_YNOP "v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
 #endif
 }
 template <int kImm, class V>
@@ -288,7 +301,8 @@ struct QSched {
   static_assert(extra_reads(kGb) == 0, "no read beside the barrier");
 };
 
-// d = a . b(AGPR) + c (c a separate VGPR tile: the dP^T chain's -Delta seeds)
+// d = a . b(AGPR) + c (c a separate VGPR tile: the dP^T chain's -Delta seeds, which hipcc
+// assembles with v_movs right before this MFMA: always padded)
 template <class T>
 __device__ __forceinline__ void mf_cacc(f32x16& d, const typename T::vec8& a, const typename T::vec8& b,
                                         const f32x16& c) {
@@ -335,6 +349,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
   __shared__ __attribute__((aligned(16))) uint8_t smem[S::kLdsBytes];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + S::kListOff);
   int* list_n = reinterpret_cast<int*>(smem + S::kListOff + 2 * kMaxBlocks);
+  int* chunk_n = list_n + 4;   // per-64-block chunk counts of the list build
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -383,20 +398,33 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
   }
   const int qlo = kPooled ? split * nbq / p.psplit : 0;
   const int qhi = kPooled ? (split + 1) * nbq / p.psplit : nbq;
-  if (threadIdx.x < 64) {   // the q-blocks that keep this key block
-    int n = 0;
-    for (int i0 = qlo; i0 < qhi; i0 += 64) {
-      const int i = i0 + lane;
+  {   // the q-blocks that keep this key block, ascending: the four waves ballot 64-block chunks
+      // wave, wave + 4, .. in one round of mask loads, then place their entries after the counts of
+      // the chunks before them (a single wave's serial loop waited for one load round per chunk)
+    constexpr int kCPW = kMaxBlocks / 64 / 4;   // chunks per wave
+    unsigned long long bal[kCPW];
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) {
+      const int i = qlo + 64 * (wave + 4 * r) + lane;
       const bool keep = (i < qhi) && (mcol == nullptr || mcol[(int64_t)i * p.ms[2]] != 0);
-      const unsigned long long bal = __ballot(keep);
-      if (keep) {
-        const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-        list[pos] = (uint16_t)i;
-      }
-      n += __popcll(bal);
+      bal[r] = __ballot(keep);
+      if (lane == 0) chunk_n[wave + 4 * r] = __popcll(bal[r]);
     }
-    if (lane == 0) *list_n = n;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) {
+      const int c = wave + 4 * r;
+      int base = 0;
+      for (int c2 = 0; c2 < c; ++c2) base += chunk_n[c2];
+      if ((bal[r] >> lane) & 1)
+        list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal[r] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal[r], 0u))] =
+            (uint16_t)(qlo + 64 * c + lane);
+    }
+    if (threadIdx.x == 0) {
+      int n = 0;
+      for (int c = 0; c < 4 * kCPW; ++c) n += chunk_n[c];
+      *list_n = n;
+    }
   }
 
   // this wave's 32 keys as B operands (lane = key, d = 16 ks + 8 half + 0..7), held in AGPRs
@@ -660,10 +688,10 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
         }
         if constexpr (mode != 2 && g == S::kGb) {
           VB_WAIT_VMCNT(kPieces);   // tile t+1 landed (tile t+2 may be in flight)
-          __builtin_amdgcn_s_barrier();
+          if constexpr (!(VB_KV_ABL & 4)) __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
         }
-        if constexpr (mode != 2 && g >= S::kDma0 && g < S::kDma0 + kPieces) piece(dn, up, g - S::kDma0);
+        if constexpr (!(VB_KV_ABL & 16) && mode != 2 && g >= S::kDma0 && g < S::kDma0 + kPieces) piece(dn, up, g - S::kDma0);
         if constexpr (g == N - 1) {
 #pragma unroll
           for (int q = 0; q < kLA; ++q) launder(nx[q]);
