@@ -1,7 +1,7 @@
 #!/bin/bash
 # Backward pipeline kernels: parity with every new kernel on, A/B against the previous kernels, traces.
 set -o pipefail
-O=gpurun_out/${TAG:-kv6}
+O=gpurun_out/${TAG:-bwd_ab}
 mkdir -p $O
 export TMPDIR=/tmp
 VB_BWD_KV64=1 VB_BWD_DQ128=1 VB_BWD_DQ64=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_backward.py tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1

@@ -2,7 +2,7 @@
 # Is the D=128 dK/dV pipeline waiting on memory? A/B against a build without DMA after the
 # prologue (wrong results, timing only), and L2 hit/miss + fetch counters of the backward.
 set -o pipefail
-O=gpurun_out/${TAG:-kv7}
+O=gpurun_out/${TAG:-bwd_l2}
 mkdir -p $O
 export TMPDIR=/tmp
 AB="cur nodma" AB_ARGS="--what bwd --variant wan" bash tools/gpu/ab.sh > $O/ab_wan.log 2>&1 || exit 1
