@@ -94,9 +94,9 @@ def test_pipeline_dkdv_agrees_with_round3_kernel(D, monkeypatch):
 
 
 @pytest.mark.parametrize("D", [64, 128])
-def test_pipeline_dq_opt_in_matches_default(D, monkeypatch):
-    """The opt-in hand-scheduled dQ (VB_BWD_DQ64/128=1; measured slower) stays correct:
-    against the default dQ kernel on a ragged length with a partial last key tile."""
+def test_pipeline_dq_agrees_with_round3_kernel(D, monkeypatch):
+    """The hand-scheduled dQ (default at D=64, opt-in VB_BWD_DQ128=1 at D=128) stays correct:
+    against the round-3 dQ kernel (VB_BWD_DQ64/128=0) on a ragged length with a partial last key tile."""
     B, H, L = 1, 2, 517
     q, k, v, do = (_rand(B, H, L, D, seed=30 + s) for s in range(4))
     nb = (L + 127) // 128

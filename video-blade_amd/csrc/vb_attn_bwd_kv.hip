@@ -37,7 +37,7 @@
 #define VB_BWD_DQ128_DEFAULT 0
 #endif
 #ifndef VB_BWD_DQ64_DEFAULT
-#define VB_BWD_DQ64_DEFAULT 0
+#define VB_BWD_DQ64_DEFAULT 1
 #endif
 #ifndef VB_BWD_KV64_DEFAULT
 #define VB_BWD_KV64_DEFAULT 1
