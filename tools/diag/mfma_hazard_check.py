@@ -1,11 +1,13 @@
-"""Static check of the VALU-write -> MFMA-read hazard for inline-asm MFMAs (vb_attn_bwd_kv.hip).
+"""Static check of the VALU <-> MFMA register hazards of inline-asm MFMAs (vb_attn_bwd_kv.hip).
 
 hipcc pads the wait states a VALU write needs before an MFMA reads the same register (2 on gfx950)
 only for the MFMAs it generates; an MFMA written in inline asm is invisible to that pass. This tool
 walks the kernel's control-flow graph (tools/diag/lgkm_check.py's block parser) and, for every
 v_mfma, looks back over the instructions issued just before it (each instruction is one wait state,
 `s_nop N` is N+1) on every path; a VALU instruction (v_*, other than an MFMA) that writes one of the
-MFMA's source registers within WAIT_STATES is reported.
+MFMA's source registers within WAIT_STATES is reported. It also reports, within a block, a VALU that
+reads or writes a register an MFMA wrote fewer than XDL_WAIT wait states before it (the
+MFMA-result hazard, likewise padded by hipcc only for its own MFMAs).
 
 Usage: python tools/diag/mfma_hazard_check.py <file.s> <kernel symbol>
 """
@@ -16,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from lgkm_check import blocks_of, regs  # noqa: E402
 
 WAIT_STATES = 2
+XDL_WAIT = 19
 
 
 def operands(rest):
@@ -100,10 +103,30 @@ def check(path, name, verbose=True):
                             bad.setdefault(ln, f"line {ln + 1}: {op} reads {sorted(dst & srcs)[:4]} written by "
                                                f"{pop} at line {pl + 1}, {ws} wait states before")
                     ws += (int(prest) + 1) if pop == "s_nop" and prest.isdigit() else 1
+    # MFMA write -> VALU access: the VALU must come >= XDL_WAIT wait states after an asm MFMA that
+    # writes a register it reads or writes (19 covers the 16-pass case). An MFMA's own issue holds
+    # its wave for >= 8 cycles (the microbenchmark's issue hold), so each one counts 8 here.
+    for bi, (_, ins, _) in enumerate(blocks):
+        for k, (ln, op, rest) in enumerate(ins):
+            if not op.startswith("v_") or op.startswith("v_mfma"):
+                continue
+            used = regs(rest)
+            ws = 0
+            for pl, pop, prest in reversed(ins[:k]):
+                if ws >= XDL_WAIT:
+                    break
+                if pop.startswith("v_mfma"):
+                    dst = regs(operands(prest)[0])
+                    if dst & used:
+                        bad.setdefault(ln, f"line {ln + 1}: {op} touches {sorted(dst & used)[:4]} written by the MFMA "
+                                           f"at line {pl + 1}, {ws} wait states before")
+                    ws += 8
+                else:
+                    ws += (int(prest) + 1) if pop == "s_nop" and prest.isdigit() else 1
     if verbose:
         for ln in sorted(bad)[:20]:
             print(bad[ln])
-        print(f"{name}: {n_mfma} MFMAs, {len(bad)} VALU->MFMA hazards")
+        print(f"{name}: {n_mfma} MFMAs, {len(bad)} hazards (VALU->MFMA and MFMA->VALU)")
     return len(bad)
 
 
