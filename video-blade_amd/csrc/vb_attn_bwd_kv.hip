@@ -274,7 +274,7 @@ struct QSched {
   static constexpr int kKOff = 0;
   static constexpr int kVOff = 4 * kTileBytes;
   static constexpr int kListOff = 8 * kTileBytes;
-  static constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16;
+  static constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16 + 4 * (bwd::kMaxBlocks / 64);
   static constexpr int kPQ = kTileBytes / 1024 / 4;
   static constexpr int kPieces = 2 * kPQ;
   static constexpr int kRpp = 1024 / RB;
@@ -398,6 +398,23 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
   }
   const int qlo = kPooled ? split * nbq / p.psplit : 0;
   const int qhi = kPooled ? (split + 1) * nbq / p.psplit : nbq;
+  // this wave's 32 keys as B operands (lane = key, d = 16 ks + 8 half + 0..7), held in AGPRs; loaded
+  // first, so their latency overlaps the list build's mask loads
+  const int key = k0 + wave * 32 + l32;
+  const bool kvalid = key < Lkey;
+  const int keyc = kvalid ? key : Lkey - 1;
+  const uint8_t* kb = kPooled
+      ? reinterpret_cast<const uint8_t*>(p.kp) + 2 * (b * p.kps[0] + h * p.kps[1] + (int64_t)keyc * p.kps[2])
+      : reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + (krow0 + keyc) * p.ks[2]);
+  const uint8_t* vb_ = kPooled
+      ? reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1] + (int64_t)keyc * p.vps[2])
+      : reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + (krow0 + keyc) * p.vs[2]);
+  V8 kf[KS], vf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = *reinterpret_cast<const V8*>(kb + (16 * s + 8 * half) * 2);
+    vf[s] = *reinterpret_cast<const V8*>(vb_ + (16 * s + 8 * half) * 2);
+  }
   {   // the q-blocks that keep this key block, ascending: the four waves ballot 64-block chunks
       // wave, wave + 4, .. in one round of mask loads, then place their entries after the counts of
       // the chunks before them (a single wave's serial loop waited for one load round per chunk)
@@ -427,22 +444,6 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     }
   }
 
-  // this wave's 32 keys as B operands (lane = key, d = 16 ks + 8 half + 0..7), held in AGPRs
-  const int key = k0 + wave * 32 + l32;
-  const bool kvalid = key < Lkey;
-  const int keyc = kvalid ? key : Lkey - 1;
-  const uint8_t* kb = kPooled
-      ? reinterpret_cast<const uint8_t*>(p.kp) + 2 * (b * p.kps[0] + h * p.kps[1] + (int64_t)keyc * p.kps[2])
-      : reinterpret_cast<const uint8_t*>(p.k) + 2 * (b * p.ks[0] + h * p.ks[1] + (krow0 + keyc) * p.ks[2]);
-  const uint8_t* vb_ = kPooled
-      ? reinterpret_cast<const uint8_t*>(p.vp) + 2 * (b * p.vps[0] + h * p.vps[1] + (int64_t)keyc * p.vps[2])
-      : reinterpret_cast<const uint8_t*>(p.v) + 2 * (b * p.vs[0] + h * p.vs[1] + (krow0 + keyc) * p.vs[2]);
-  V8 kf[KS], vf[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    kf[s] = *reinterpret_cast<const V8*>(kb + (16 * s + 8 * half) * 2);
-    vf[s] = *reinterpret_cast<const V8*>(vb_ + (16 * s + 8 * half) * 2);
-  }
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     to_agpr(kf[s]);
@@ -828,7 +829,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
   constexpr int kPieces = S::kPieces, kPQ = S::kPQ;
   __shared__ __attribute__((aligned(16))) uint8_t smem[S::kLdsBytes];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + S::kListOff);
-  int* list_n = reinterpret_cast<int*>(smem + S::kListOff + 2 * kMaxBlocks);
+  int* list_n = reinterpret_cast<int*>(smem + S::kListOff + 2 * kMaxBlocks);   // [4] + chunk counts
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -867,30 +868,15 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head, p.hm_mode);
     if (mh) mrow = mh + (int64_t)qblk * p.ms[2];
   }
-  if (threadIdx.x < 64) {
-    int n = 0;
-    if (use_main) {
-      for (int j0 = 0; j0 < nbk; j0 += 64) {
-        const int j = j0 + lane;
-        const bool keep = (j < nbk) && (mrow == nullptr || mrow[j] != 0);
-        const unsigned long long bal = __ballot(keep);
-        if (keep) {
-          const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-          list[pos] = (uint16_t)j;
-        }
-        n += __popcll(bal);
-      }
-    }
-    if (lane == 0) *list_n = n;
-  }
 
   // this wave's 32 query rows: Q and dO as B operands (lane = query), held in AGPRs
   const int g = q0 + wave * 32 + l32;
   const bool qvalid = g < Lq;
   const int gc = qvalid ? g : Lq - 1;
   V8 qf[KS], df[KS];
-  {
+  const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
+  const float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];   // D1, D2 = -Delta
+  {   // (these loads first: their latency overlaps the list build's mask loads)
     const uint8_t* qp = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + (qrow0 + gc) * p.qs[2]);
     const uint8_t* dp_ = reinterpret_cast<const uint8_t*>(p.dout) + 2 * (b * p.dos[0] + h * p.dos[1] + (qrow0 + gc) * p.dos[2]);
 #pragma unroll
@@ -898,15 +884,41 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
       qf[s] = *reinterpret_cast<const V8*>(qp + (16 * s + 8 * half) * 2);
       df[s] = *reinterpret_cast<const V8*>(dp_ + (16 * s + 8 * half) * 2);
     }
+    {   // the kept key blocks, ascending: the four waves ballot 64-block chunks wave, wave + 4, .. in
+        // one round of mask loads, then place their entries after the counts of the chunks before them
+      constexpr int kCPW = kMaxBlocks / 64 / 4;
+      int* chunk_n = list_n + 4;
+      unsigned long long bal[kCPW];
+#pragma unroll
+      for (int r = 0; r < kCPW; ++r) {
+        const int j = 64 * (wave + 4 * r) + lane;
+        const bool keep = use_main && (j < nbk) && (mrow == nullptr || mrow[j] != 0);
+        bal[r] = __ballot(keep);
+        if (lane == 0) chunk_n[wave + 4 * r] = __popcll(bal[r]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kCPW; ++r) {
+        const int c = wave + 4 * r;
+        int base = 0;
+        for (int c2 = 0; c2 < c; ++c2) base += chunk_n[c2];
+        if ((bal[r] >> lane) & 1)
+          list[base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal[r] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal[r], 0u))] =
+              (uint16_t)(64 * c + lane);
+      }
+      if (threadIdx.x == 0) {
+        int n = 0;
+        for (int c = 0; c < 4 * kCPW; ++c) n += chunk_n[c];
+        *list_n = n;
+      }
+    }
+
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       to_agpr(qf[s]);
       to_agpr(df[s]);
     }
   }
-  const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
-  const float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];   // D1, D2 = -Delta
-
   __syncthreads();
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
   int ntm = 2 * nkept;
