@@ -4,7 +4,9 @@ ONE GPU: the same inputs, launches interleaved A,B,A,B,... so clock/device drift
 usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred|call]
 TAG "cur" is the in-tree libvblade_hip.so; a "@torchrand" suffix runs that tag with the sampling
 draws made by torch.rand instead of inside the sampling launch (ops.PHILOX_DRAWS off), "@lvsep"
-with the multi-level mask as its own vb_level_mask launch (--what mlcall: the multi-level module)."""
+with the multi-level mask as its own vb_level_mask launch (--what mlcall: the multi-level module),
+"@env:VAR=VAL+VAR=VAL" with those environment variables set around its launches (the library reads
+its VB_BWD_* switches per call)."""
 import argparse
 import ctypes
 import os
@@ -35,6 +37,25 @@ def load(tag):
             continue
         fn.restype, fn.argtypes = res, args
     return lib
+
+
+def select(tag, libs):
+    """make `tag` the active variant: its library, its module switches and its environment"""
+    _lib._lib = libs[tag]
+    ops.PHILOX_DRAWS = "@torchrand" not in tag
+    multilevel.FUSED_LEVEL_MASK = "@lvsep" not in tag
+    for kv in ENV_SET:
+        os.environ.pop(kv, None)
+    ENV_SET.clear()
+    for part in tag.split("@")[1:]:
+        if part.startswith("env:"):
+            for kv in part[4:].split("+"):
+                k, v = kv.split("=", 1)
+                os.environ[k] = v
+                ENV_SET.append(k)
+
+
+ENV_SET = []
 
 
 def main():
@@ -97,9 +118,7 @@ def main():
         times = {kk: [] for kk in keys}
         with torch.no_grad():
             for t in a.tags:   # warm + cross-check outputs (a repeated tag checks determinism)
-                _lib._lib = libs[t]
-                ops.PHILOX_DRAWS = not t.endswith("@torchrand")
-                multilevel.FUSED_LEVEL_MASK = not t.endswith("@lvsep")
+                select(t, libs)
                 out = fn()
                 torch.cuda.synchronize()
                 if a.what == "pred":   # the same scores and energy rule: masks must be identical
@@ -120,9 +139,7 @@ def main():
                               f"max|diff| = {err:.3e}; per output max|diff|/max|ref| = {rel}")
             for _ in range(a.rounds):
                 for kk, t in zip(keys, a.tags):
-                    _lib._lib = libs[t]
-                    ops.PHILOX_DRAWS = not t.endswith("@torchrand")
-                    multilevel.FUSED_LEVEL_MASK = not t.endswith("@lvsep")
+                    select(t, libs)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(5):

@@ -979,7 +979,14 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
       return d;
     };
     auto piece = [&](const TileDma& d, int slot, int k) __attribute__((always_inline)) {
-      const int vo = d.pooled ? opaque(voff_p[k]) : opaque(voff_m[k]);
+      int vo = voff_m[k];
+      if constexpr (kPool) {   // one v_bfi on a uniform mask; a select here becomes a branch per piece
+        int pm = uniform(d.pooled ? -1 : 0);
+#if __HIP_DEVICE_COMPILE__
+        asm volatile("" : "+s"(pm));
+#endif
+        vo = (pm & voff_p[k]) | (~pm & vo);
+      }
       if (k < kPQ) dma16(d.k, smem + S::kKOff + slot * TB + (wave + 4 * k) * 1024, vo, d.soff_k);
       else dma16(d.v, smem + S::kVOff + slot * TB + (wave + 4 * (k - kPQ)) * 1024, vo, d.soff_v);
     };
@@ -1022,6 +1029,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
       const float dr = pooled ? opaque(D2) : opaque(D1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) cdt[r] = dr;
+      launder(cdt);   // kept in 16 registers: hipcc would rebuild the broadcast with 16 v_movs per tile
       nl0 = pooled ? -opaque(L2) : -opaque(L1);
     };
 
@@ -1124,7 +1132,10 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
         if constexpr (g == N - 1) {
 #pragma unroll
           for (int q = 0; q < kLA; ++q) launder(nx[q]);
-          if constexpr (mode != 2) set_class(kPool && t + 1 >= ntm);   // tile t+1's seeds and -L'
+          // tile t+1's seeds and -L': they change once, at the first pooled tile
+          if constexpr (mode != 2 && kPool) {
+            if (t + 1 == ntm) set_class(true);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       };
