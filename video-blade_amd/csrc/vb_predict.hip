@@ -34,7 +34,15 @@ constexpr int kEnergyRow = kMaxNb + 16;   // LDS floats per energy-rule row buff
 // keys per LDS tile: D=64 streams four 32-key sampled blocks per barrier (16 MFMAs per wave),
 // D=128 two (also 16 MFMAs); 16 KiB tiles in a 2-deep ring at D=64 (36.5 KiB with the row-offset
 // ring: four workgroups per CU) and a 3-deep ring at D=128 (52.5 KiB: three per CU)
-template <int D> constexpr int kKeysPerTile = (D == 64) ? 128 : 64;
+#ifndef VB_PRED_QPW64
+#define VB_PRED_QPW64 1   // D=64: sampled q-blocks per wave (2: each K fragment read feeds two MFMAs)
+#endif
+template <int D> constexpr int kQPW = D == 64 ? VB_PRED_QPW64 : 1;
+// (with two q-blocks per wave the tile halves: the same 16 MFMAs per wave and barrier)
+#ifndef VB_PRED_KPT64
+#define VB_PRED_KPT64 (128 / VB_PRED_QPW64)   // D=64 keys per LDS tile
+#endif
+template <int D> constexpr int kKeysPerTile = (D == 64) ? VB_PRED_KPT64 : 64;
 #ifndef VB_PRED_BUFS
 #define VB_PRED_BUFS 3
 #endif
@@ -433,7 +441,8 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
   constexpr int kRowsPerInst = 1024 / kRowB;          // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerWave = kTileBytes / 1024 / kPWaves;
   constexpr int kBufs = kPBufs<D>;                    // tile t read, the younger ones in flight
-  constexpr int kSt = kKT / 2;                        // R stores per wave and tile
+  constexpr int KQ = kQPW<D>;                         // sampled q-blocks per wave
+  constexpr int kSt = KQ * (kKT / 2);                 // R stores per wave and tile
   // LDS: m [4][32] f32 | K tiles x4 (after the main loop: per-wave row scratch). The per-row
   // block maxima R go to a global scratch in [key block][32 rows] order (as the Triton kernel keeps
   // R in HBM): a tile's two columns are one contiguous 128-byte store, and the LDS stays small
@@ -461,7 +470,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nb = p.nb;
   float* mrow_s = reinterpret_cast<float*>(smem);
-  uint8_t* ktile = smem + kPWaves * 32 * 4;
+  uint8_t* ktile = smem + kPWaves * KQ * 32 * 4;
   float* rowbuf = reinterpret_cast<float*>(ktile);  // [4][2][kEnergyRow], reused after the loop
 
   const int lane = threadIdx.x & 63;
@@ -470,27 +479,29 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
   const int l32 = lane & 31;
   // XCD-aware order: give each XCD a contiguous range of (head, q-group) work, so a head's sampled
   // keys are re-read from that XCD's own L2. Placement only affects speed.
-  const int nqg = (nb + kPWaves - 1) / kPWaves;
+  const int nqg = (nb + kPWaves * KQ - 1) / (kPWaves * KQ);
   const int lin = xcd_linear(wg, nqg * p.B * p.H);
   const int bh = lin / nqg;
-  const int qb = (lin % nqg) * kPWaves + wave;  // this wave's sampled q-block
-  const bool wave_active = qb < nb;
+  int qbs[KQ];   // this wave's sampled q-blocks
+#pragma unroll
+  for (int e = 0; e < KQ; ++e) qbs[e] = (lin % nqg) * kPWaves * KQ + wave * KQ + e;
 #if !VB_PRED_GATHER
   const int64_t slice = (int64_t)nb * 32 * kRowB;   // bytes of one (b,h) sampled stream
 #endif
 
   // Q fragment of this lane's sampled row (B operand of S^T = K_s . Q_s^T), gathered straight from
   // the caller's q: reordered-padded position qb*block + q_off[l32] (replicate padding) at row rows[pos]
-  typename T::vec8 qf[KS];
-  {
+  typename T::vec8 qf[KQ][KS];
+#pragma unroll
+  for (int e = 0; e < KQ; ++e) {
     const int b = bh / p.H, h = bh % p.H;
-    const int qrow = sampled_row(wave_active ? qb : 0, p.q_off[(int64_t)bh * 32 + l32], p.block, p.L, p.rows);
+    const int qrow = sampled_row(qbs[e] < nb ? qbs[e] : 0, p.q_off[(int64_t)bh * 32 + l32], p.block, p.L, p.rows);
     const uint8_t* qp = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + (int64_t)qrow * p.qs[2]);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      qf[s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
+      qf[e][s] = *reinterpret_cast<const typename T::vec8*>(qp + (16 * s + 8 * half) * 2);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]));  // see vb_attn_fwd.hip
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[e][s]));  // see vb_attn_fwd.hip
   }
   // K tiles by LDS-DMA from the contiguous sampled stream: a buffer descriptor per (b,h), each
   // lane's fixed (row, swizzled chunk) as voffset, the tile's first row as soffset. Rows past the
@@ -528,7 +539,9 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     voff[i] = r * kRowB + 16 * (sl ^ sw);
   }
 #endif
-  float m = -INFINITY;
+  float m[KQ];
+#pragma unroll
+  for (int e = 0; e < KQ; ++e) m[e] = -INFINITY;
   __syncthreads();   // all plain global loads retired before the DMA pipeline
 
   const int ntiles = (VB_DIAG && (p.dbg & 2)) ? 0 : (nb + kKT - 1) / kKT;
@@ -567,8 +580,13 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     const int sw = (D == 64) ? ((l32 >> 1) & 7) : (l32 & 15);
     k_lane[ks] = l32 * kRowB + 16 * ((2 * ks + half) ^ sw);
   }
-  uint16_t* Rq = p.rbuf + ((int64_t)bh * nb + (wave_active ? qb : 0)) * nb * 32;   // this q-block
-  const srd_t rsrd = make_srd(Rq, wave_active ? nb * 64 : 0);
+  uint16_t* Rqs[KQ];   // this wave's q-blocks' R slices
+  srd_t rsrd[KQ];
+#pragma unroll
+  for (int e = 0; e < KQ; ++e) {
+    Rqs[e] = p.rbuf + ((int64_t)bh * nb + (qbs[e] < nb ? qbs[e] : 0)) * nb * 32;
+    rsrd[e] = make_srd(Rqs[e], qbs[e] < nb ? nb * 64 : 0);
+  }
 #if VB_PRED_GATHER
   // Issue order: I0 I1 I2 K0 K1, then per body t: I(t+3) K(t+2) [compute] S(t) — every DMA is
   // issued, past the last tile too (offsets past the table read 0: row 0 into a slot no tile reads
@@ -646,7 +664,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     if (VB_DIAG && (p.dbg & 4)) return;   // diagnostic: stream the K tiles only
     // one accumulator per 32-key block: the MFMAs of block kt+1 do not wait for the row-max
     // reads of block kt (a shared accumulator serialises MFMA -> s_nop -> VALU -> MFMA)
-    f32x16 sc[kKT];
+    f32x16 sc[KQ][kKT];
 #pragma unroll
     for (int kt = 0; kt < kKT; ++kt) {
       typename T::vec8 kf[KS];
@@ -654,9 +672,13 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
       for (int ks = 0; ks < KS; ++ks)
         kf[ks] = *reinterpret_cast<const typename T::vec8*>(kl + kt * 32 * kRowB + k_lane[ks]);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
+      for (int e = 0; e < KQ; ++e)
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) sc[kt] = T::mfma32(kf[ks], qf[ks], sc[kt]);
+        for (int r = 0; r < 16; ++r) sc[e][kt][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int e = 0; e < KQ; ++e) sc[e][kt] = T::mfma32(kf[ks], qf[e][ks], sc[e][kt]);
     }
 #if VB_PRED_SCHED
     // Pin the issue order: each K-fragment read VB_PRED_SCHED MFMAs ahead of the MFMA that consumes
@@ -665,20 +687,22 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     for (int i = 0; i < VB_PRED_SCHED; ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
 #pragma unroll
     for (int i = 0; i < kKT * KS; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, KQ, 0);
       if (i + VB_PRED_SCHED < kKT * KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
 #endif
     // row maxima, two 32-key blocks per v_permlane32_swap: after the swap lanes 0-31 hold block
     // 2pr's full row max and lanes 32-63 block 2pr+1's (the halves of each block's C tile meet)
     const int j0 = kKT * t;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
     float mxp[kKT / 2];
 #pragma unroll
     for (int pr = 0; pr < kKT / 2; ++pr) {
       float x[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const f32x16& a = sc[2 * pr + e];
+        const f32x16& a = sc[q][2 * pr + e];
         float y = fmaxf(fmaxf(a[0], a[1]), a[2]);
 #pragma unroll
         for (int r = 3; r < 15; r += 2) y = fmaxf(fmaxf(y, a[r]), a[r + 1]);
@@ -694,13 +718,14 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
         if (j0 + 2 * pr + half >= nb) mxp[pr] = -INFINITY;
     }
 #pragma unroll
-    for (int pr = 0; pr < kKT / 2; ++pr) m = fmaxf(m, mxp[pr]);   // this half's blocks; halves meet below
+    for (int pr = 0; pr < kKT / 2; ++pr) m[q] = fmaxf(m[q], mxp[pr]);   // this half's blocks; halves meet below
     // R[j][row]: lane (half, row) stores block j0 + 2pr + half, so one store writes 128 contiguous
     // bytes. Issued unconditionally (kSt per body, the vmcnt arithmetic above relies on it): blocks
-    // past nb fall outside the descriptor and an inactive wave's descriptor is empty, so the
+    // past nb fall outside the descriptor and an inactive q-block's descriptor is empty, so the
     // hardware drops those lanes.
 #pragma unroll
-    for (int pr = 0; pr < kSt; ++pr) store16(rsrd, (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
+    for (int pr = 0; pr < kKT / 2; ++pr) store16(rsrd[q], (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
+    }
 #if VB_PRED_STAMPS
     VB_PST(b4);
     pst[3] += b4 - b0;
@@ -721,85 +746,93 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
 #if VB_PRED_STAMPS
   VB_PST(e0);
 #endif
-  m = max_xor32(m);   // the two halves saw alternate key blocks
-  if (half == 0) mrow_s[wave * 32 + l32] = m;
+#pragma unroll
+  for (int e = 0; e < KQ; ++e) {
+    m[e] = max_xor32(m[e]);   // the two halves saw alternate key blocks
+    if (half == 0) mrow_s[(wave * KQ + e) * 32 + l32] = m[e];
+  }
   __syncthreads();
-  if (!wave_active || (VB_DIAG && (p.dbg & 1))) return;
+  if (VB_DIAG && (p.dbg & 1)) return;
 
   // Po[qb, j] = storage(max_r exp2(R[r][j] - m_r)) = storage(exp2(max_r (R[r][j] - m_r)))
-  // (exp2 and the rounding are monotone), then the storage-dtype row normalisation
+  // (exp2 and the rounding are monotone), then the storage-dtype row normalisation; one q-block
+  // after the other (the wave's row scratch is reused)
   float* val = rowbuf + wave * 2 * (kEnergyRow);
   uint32_t* keys = reinterpret_cast<uint32_t*>(val + kEnergyRow);
-  const float* mw = mrow_s + wave * 32;
-  // this wave's R columns were stored by its own lanes: wait for them and drop any stale L1 line
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  float mreg[32];
+  auto epilogue = [&](const int qb, const uint16_t* Rq, const float* mw) __attribute__((always_inline)) {
+    // this wave's R columns were stored by its own lanes: wait for them and drop any stale L1 line
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    float mreg[32];
 #pragma unroll
-  for (int r = 0; r < 32; r += 4) {
-    const f32x4 x = *reinterpret_cast<const f32x4*>(mw + r);
+    for (int r = 0; r < 32; r += 4) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(mw + r);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) mreg[r + e] = x[e];
-  }
-  float part = 0.f;
-  // VB_PRED_RCOLS columns per lane per pass (4 loads each in flight): the block's 32 row maxima
-  // are 64 contiguous bytes
-  constexpr int kRC = VB_PRED_RCOLS;
-  for (int j0 = 0; j0 < nb; j0 += 64 * kRC) {
-    u32x4 w[kRC][4];
-#pragma unroll
-    for (int h = 0; h < kRC; ++h) {
-      const int jj = min(j0 + 64 * h + lane, nb - 1);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) w[h][c] = reinterpret_cast<const u32x4*>(Rq + jj * 32)[c];
+      for (int e = 0; e < 4; ++e) mreg[r + e] = x[e];
     }
+    float part = 0.f;
+    // VB_PRED_RCOLS columns per lane per pass (4 loads each in flight): the block's 32 row maxima
+    // are 64 contiguous bytes
+    constexpr int kRC = VB_PRED_RCOLS;
+    for (int j0 = 0; j0 < nb; j0 += 64 * kRC) {
+      u32x4 w[kRC][4];
 #pragma unroll
-    for (int h = 0; h < kRC; ++h) {
-      const int j = j0 + 64 * h + lane;
-      float cm = -INFINITY;
+      for (int h = 0; h < kRC; ++h) {
+        const int jj = min(j0 + 64 * h + lane, nb - 1);
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < 4; ++c) w[h][c] = reinterpret_cast<const u32x4*>(Rq + jj * 32)[c];
+      }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 8 * c + 2 * e;
-          cm = max3f(cm, T::bits_to_f32((uint16_t)(w[h][c][e] & 0xFFFF)) - mreg[r],
-                     T::bits_to_f32((uint16_t)(w[h][c][e] >> 16)) - mreg[r + 1]);
+      for (int h = 0; h < kRC; ++h) {
+        const int j = j0 + 64 * h + lane;
+        float cm = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * c + 2 * e;
+            cm = max3f(cm, T::bits_to_f32((uint16_t)(w[h][c][e] & 0xFFFF)) - mreg[r],
+                       T::bits_to_f32((uint16_t)(w[h][c][e] >> 16)) - mreg[r + 1]);
+          }
+        cm = round_to<T>(exp2_fast(cm));
+        if (j < nb) {
+          val[j] = cm;
+          part += cm;
         }
-      cm = round_to<T>(exp2_fast(cm));
-      if (j < nb) {
-        val[j] = cm;
-        part += cm;
       }
     }
-  }
-  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-  const float tot = round_to<T>(part);
-  typename T::raw* po = reinterpret_cast<typename T::raw*>(p.po) + ((int64_t)bh * nb + qb) * nb;
-  for (int j = lane; j < nb; j += 64) {
-    const float v = round_to<T>(val[j] / tot);
-    val[j] = v;
-    po[j] = T::from_f32(v);
-  }
-#if VB_PRED_STAMPS
-  {
-    VB_PST(e1);
-    if (lane == 0) {
-      for (int i = 0; i < 4; ++i) atomicAdd(&g_pred_stamp[i], pst[i]);
-      atomicAdd(&g_pred_stamp[4], e1 - e0);
-      atomicAdd(&g_pred_stamp[5], 1ull);
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    const float tot = round_to<T>(part);
+    typename T::raw* po = reinterpret_cast<typename T::raw*>(p.po) + ((int64_t)bh * nb + qb) * nb;
+    for (int j = lane; j < nb; j += 64) {
+      const float v = round_to<T>(val[j] / tot);
+      val[j] = v;
+      po[j] = T::from_f32(v);
     }
-  }
+#if VB_PRED_STAMPS
+    {
+      VB_PST(e1);
+      if (lane == 0) {
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_pred_stamp[i], pst[i]);
+        atomicAdd(&g_pred_stamp[4], e1 - e0);
+        atomicAdd(&g_pred_stamp[5], 1ull);
+      }
+    }
 #endif
-  if (!kEnergy || p.mask == nullptr) return;   // scores only (energy rule elsewhere / not wanted)
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  uint8_t* mrow = p.mask + ((int64_t)bh * nb + qb) * nb;
-  if (p.level) {   // the multi-level path's rank bands instead of the energy rule
-    level_row<T>(val, keys, mrow, nb, qb, p.lv);
-    return;
-  }
-  const bool force_all = p.force_tail > 0 && qb >= nb - p.force_tail;
-  const int kept = energy_row<T>(val, keys, mrow, nb, p.thr, p.min_keep, p.max_keep, p.force_tail, force_all);
-  if (p.count && lane == 0) atomicAdd(p.count, (unsigned long long)kept);
+    if (!kEnergy || p.mask == nullptr) return;   // scores only (energy rule elsewhere / not wanted)
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    uint8_t* mrow = p.mask + ((int64_t)bh * nb + qb) * nb;
+    if (p.level) {   // the multi-level path's rank bands instead of the energy rule
+      level_row<T>(val, keys, mrow, nb, qb, p.lv);
+      return;
+    }
+    const bool force_all = p.force_tail > 0 && qb >= nb - p.force_tail;
+    const int kept = energy_row<T>(val, keys, mrow, nb, p.thr, p.min_keep, p.max_keep, p.force_tail, force_all);
+    if (p.count && lane == 0) atomicAdd(p.count, (unsigned long long)kept);
+  };
+#pragma unroll
+  for (int e = 0; e < KQ; ++e)
+    if (qbs[e] < nb) epilogue(qbs[e], Rqs[e], mrow_s + (wave * KQ + e) * 32);
 }
 
 // random_sample_tokens' topk (cogvideo_blocksparseattn.py:45-46): for every row of `n` uniform draws,
@@ -840,7 +873,8 @@ static size_t predict_smem_bytes(int nb, int D) {
                                : (size_t)kPBufs<128> * kKeysPerTile<128> * 128 * 2;
   const size_t scratch = (size_t)kPWaves * 2 * (kEnergyRow) * 4;
   const size_t ring = VB_PRED_GATHER ? 4 * kPWaves * 256 : 0;   // gather mode: the row-offset ring
-  return kPWaves * 32 * 4 + (tiles + ring > scratch ? tiles + ring : scratch);
+  const size_t mrow = (size_t)kPWaves * (D == 64 ? kQPW<64> : kQPW<128>) * 32 * 4;
+  return mrow + (tiles + ring > scratch ? tiles + ring : scratch);
 }
 
 // workspace: sampled k rows (gather mode: their int32 byte offsets) | R
@@ -879,7 +913,8 @@ static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t st
                      0, stream, p);
   if (int rc = check_launch("sample_rows_kernel")) return rc;
   if (staged && hipEventRecord(staged, stream) != hipSuccess) return fail(VB_ERR_LAUNCH, "vb_mask_predict: hipEventRecord failed");
-  const dim3 grid(((p.nb + kPWaves - 1) / kPWaves) * p.B * p.H + p.n_pool);
+  constexpr int qpw = kPWaves * kQPW<D>;   // sampled q-blocks per workgroup
+  const dim3 grid(((p.nb + qpw - 1) / qpw) * p.B * p.H + p.n_pool);
   hipLaunchKernelGGL(kern, grid, dim3(kPThreads), smem, stream, p);
   if (int rc = check_launch("mask_predict_kernel")) return rc;
   if (VB_PRED_SPLIT_ENERGY && p.mask) {
