@@ -965,17 +965,37 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     // Every select below takes opaque operands (readfirstlane / an empty asm): hipcc otherwise turns
     // a select between two loads of captured locals into a load through a selected address, which
     // moves those locals to scratch.
+    // The pooled variant blends the main and pooled sources with a uniform mask (x ^ ((x ^ y) & pm))
+    // of values made uniform once, here: a select between them compiles to a branch per field.
+    struct Src {
+      uint32_t klo, khi, vlo, vhi;
+      int kbytes, vbytes, krowb, vrowb;
+    };
+    auto src_of = [](const uint8_t* kb, const uint8_t* vb, int kby, int vby, int krb, int vrb) -> Src {
+      const uint64_t k = reinterpret_cast<uint64_t>(kb), v = reinterpret_cast<uint64_t>(vb);
+      return Src{(uint32_t)uniform((int)(uint32_t)k), (uint32_t)uniform((int)(uint32_t)(k >> 32)),
+                 (uint32_t)uniform((int)(uint32_t)v), (uint32_t)uniform((int)(uint32_t)(v >> 32)),
+                 uniform(kby), uniform(vby), uniform(krb), uniform(vrb)};
+    };
+    const Src sm = src_of(kbase, vbase, kbytes, vbytes, krowb, vrowb);
+    Src sx{};   // main ^ pooled
+    if constexpr (kPool) {
+      const Src sp = src_of(kpbase, vpbase, kpbytes, vpbytes, kprowb, vprowb);
+      sx = Src{sm.klo ^ sp.klo, sm.khi ^ sp.khi, sm.vlo ^ sp.vlo, sm.vhi ^ sp.vhi,
+               sm.kbytes ^ sp.kbytes, sm.vbytes ^ sp.vbytes, sm.krowb ^ sp.krowb, sm.vrowb ^ sp.vrowb};
+    }
     auto tile_dma = [&](int tt, int blk) __attribute__((always_inline)) -> TileDma {
       TileDma d;
       d.pooled = kPool && tt >= ntm;
-      const bool live = tt < ntiles;
+      const int pm = kPool ? -(int)(tt >= ntm) : 0;
+      const int lm = -(int)(tt < ntiles);
       const int kstart = d.pooled ? (tt - ntm) * kT : blk * kBlk + (tt & 1) * kT;
-      d.k = srd_t{d.pooled ? uniform_ptr(kpbase) : uniform_ptr(kbase),
-                  live ? (d.pooled ? uniform(kpbytes) : uniform(kbytes)) : 0};
-      d.v = srd_t{d.pooled ? uniform_ptr(vpbase) : uniform_ptr(vbase),
-                  live ? (d.pooled ? uniform(vpbytes) : uniform(vbytes)) : 0};
-      d.soff_k = kstart * (d.pooled ? uniform(kprowb) : uniform(krowb));
-      d.soff_v = kstart * (d.pooled ? uniform(vprowb) : uniform(vrowb));
+      const uint32_t klo = sm.klo ^ (sx.klo & (uint32_t)pm), khi = sm.khi ^ (sx.khi & (uint32_t)pm);
+      const uint32_t vlo = sm.vlo ^ (sx.vlo & (uint32_t)pm), vhi = sm.vhi ^ (sx.vhi & (uint32_t)pm);
+      d.k = srd_t{reinterpret_cast<const void*>(((uint64_t)khi << 32) | klo), (sm.kbytes ^ (sx.kbytes & pm)) & lm};
+      d.v = srd_t{reinterpret_cast<const void*>(((uint64_t)vhi << 32) | vlo), (sm.vbytes ^ (sx.vbytes & pm)) & lm};
+      d.soff_k = kstart * (sm.krowb ^ (sx.krowb & pm));
+      d.soff_v = kstart * (sm.vrowb ^ (sx.vrowb & pm));
       return d;
     };
     auto piece = [&](const TileDma& d, int slot, int k) __attribute__((always_inline)) {
