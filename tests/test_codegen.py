@@ -126,6 +126,33 @@ def test_kv128_no_valu_to_asm_mfma_hazard(kv128_asm, name, capsys):
     assert mfma_hazard_check.check(kv128_asm, name) == 0, capsys.readouterr().out[-2000:]
 
 
+@pytest.mark.parametrize("name", KV128_KERNELS)
+def test_pipeline_tiles_have_no_per_piece_branches(kv128_asm, name):
+    """Between two tile barriers the pipeline runs its MFMA stream with no data-dependent control
+    flow: only the loop's own exit test, and in the pooled dQ the once-per-launch switch to the
+    pooled seeds (`set_class`). A select hipcc turns into branches (the dQ's per-piece voffset and
+    per-tile descriptor choice did: 28-44 branches per window) shows up here."""
+    lines = open(kv128_asm).read().split("\n")
+    s = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
+    e = next(i for i in range(s, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    windows, mfma, br = [], 0, 0
+    for l in lines[s:e]:
+        t = l.split(";")[0].split()
+        if not t:
+            continue
+        if t[0] == "s_barrier":
+            windows.append((mfma, br))
+            mfma, br = 0, 0
+        elif t[0].startswith("v_mfma"):
+            mfma += 1
+        elif t[0].startswith("s_cbranch"):
+            br += 1
+    steady = [b for m, b in windows if m >= 8]   # windows of the tile loop
+    assert steady, "no tile windows found in " + name
+    limit = 4 if "dq_pipe" in name and name.endswith("Lb1EEEvNS_9BwdParamsE") else 1
+    assert max(steady) <= limit, (name, sorted(set(steady)))
+
+
 SYNTH = """k:
 \tds_read_b128 v[4:7], v1 offset:16
 \tv_mov_b32_e32 v9, 0
