@@ -758,7 +758,7 @@ def quality_vs_oracle(mod, qkv, variant):
     return {"head": 0, "psnr_db": psnr(got, ref),
             # how head_mask_type = ones(H) reads the predicted masks
             "mask_head_mode": mod.mask_head_mode,
-            "forward_kernel": "attn_fwd1_kernel (one wave per SIMD)" if ops.FWD1 else "attn_fwd_kernel",
+            "forward_kernel": "attn_fwd_kernel",
             "max_abs": round((got - ref).abs().max().item(), 5),
             "ulp_hist": h_ref["ulp_hist"], "max_ulp": h_ref["max_ulp"],
             "vs": "oracle/bsa_oracle.adaptive_attention (reference rounding), same mask",
@@ -795,7 +795,7 @@ def pmc_traffic(variant, timeout=300, density=None, band=False, local=False):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 kn = r.get("Kernel_Name", "")
-                if ("attn_fwd_kernel" in kn or "attn_fwd1_kernel" in kn) and r.get("Counter_Name") == counter:
+                if "attn_fwd_kernel" in kn and r.get("Counter_Name") == counter:
                     xs.append(float(r["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not xs:

@@ -178,3 +178,43 @@ def test_checkers_detect_synthetic_violations(tmp_path, capsys):
     assert lgkm_check.check(str(f), "k") == 0
     f.write_text(SYNTH.replace("v[8:11], v[12:15]", "v[4:7], v[12:15]"))
     assert lgkm_check.check(str(f), "k") == 1
+
+
+# an asm MFMA writes v[32:47] before a loop back-edge and a branch; the VALU that reads v40 sits at the
+# top of the loop body (a different block, 2 wait states after the MFMA along the back-edge)
+SYNTH_CFG = """k:
+\ts_mov_b32 s0, 4
+.LBB0_1:
+\tv_add_f32_e32 v50, v40, v41
+\ts_cmp_eq_u32 s0, 0
+\ts_cbranch_scc1 .LBB0_3
+.LBB0_2:
+\tv_mfma_f32_32x32x16_bf16 v[32:47], v[8:11], v[12:15], v[32:47]
+\ts_sub_u32 s0, s0, 1
+\ts_branch .LBB0_1
+.LBB0_3:
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+def test_hazard_checker_follows_branches_and_back_edges(tmp_path, capsys):
+    """the MFMA-result -> VALU direction walks every control-flow path (here the loop's
+    back-edge), not only the VALU's own block; padding the read far enough clears it. The swap forms
+    count both operands as destinations in the VALU -> MFMA direction."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools", "diag"))
+    import mfma_hazard_check
+    f = tmp_path / "k.s"
+    f.write_text(SYNTH_CFG)
+    assert mfma_hazard_check.check(str(f), "k") == 1
+    f.write_text(SYNTH_CFG.replace("\ts_sub_u32 s0, s0, 1\n", "\ts_sub_u32 s0, s0, 1\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n"))
+    assert mfma_hazard_check.check(str(f), "k") == 0
+    swap = """k:
+\tv_permlane32_swap_b32_e32 v20, v12
+\tv_mfma_f32_32x32x16_bf16 a[0:15], v[8:11], v[12:15], a[0:15]
+\ts_endpgm
+.Lfunc_end0:
+"""
+    f.write_text(swap)
+    assert mfma_hazard_check.check(str(f), "k") == 1

@@ -5,9 +5,11 @@ only for the MFMAs it generates; an MFMA written in inline asm is invisible to t
 walks the kernel's control-flow graph (tools/diag/lgkm_check.py's block parser) and, for every
 v_mfma, looks back over the instructions issued just before it (each instruction is one wait state,
 `s_nop N` is N+1) on every path; a VALU instruction (v_*, other than an MFMA) that writes one of the
-MFMA's source registers within WAIT_STATES is reported. It also reports, within a block, a VALU that
-reads or writes a register an MFMA wrote fewer than XDL_WAIT wait states before it (the
-MFMA-result hazard, likewise padded by hipcc only for its own MFMAs).
+MFMA's source registers within WAIT_STATES is reported. It also reports a VALU that reads or writes
+a register an MFMA wrote fewer than XDL_WAIT wait states before it on any path into it, across
+branches and loop back-edges (the MFMA-result hazard, likewise padded by hipcc only for its own
+MFMAs). VALU destinations are operand 0, plus operand 1 for the swap forms (v_permlane*_swap,
+v_swap_b32), which write both.
 
 Usage: python tools/diag/mfma_hazard_check.py <file.s> <kernel symbol>
 """
@@ -38,6 +40,27 @@ def operands(rest):
     return out
 
 
+def wait_states(item):
+    """wait states one issued instruction covers (s_nop N: N + 1)"""
+    return (int(item[2]) + 1) if item[1] == "s_nop" and item[2].isdigit() else 1
+
+
+def xdl_cost(item):
+    """as wait_states, but an MFMA's own issue holds its wave for >= 8 cycles"""
+    return 8 if item[1].startswith("v_mfma") else wait_states(item)
+
+
+def valu_dst(op, rest):
+    """VGPRs a VALU instruction writes"""
+    if not rest:
+        return frozenset()
+    ops = operands(rest)
+    dst = regs(ops[0])
+    if ("swap" in op) and len(ops) > 1:   # v_permlane16/32_swap, v_swap_b32: both operands
+        dst = dst | regs(ops[1])
+    return dst
+
+
 def check(path, name, verbose=True):
     lines = open(path).read().split("\n")
     start = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
@@ -48,9 +71,10 @@ def check(path, name, verbose=True):
         for s in succ:
             preds[s].append(i)
 
-    def tail(bi, need, seen):
+    def tail(bi, need, seen, cost=wait_states):
         """instructions (line, op, rest) of the paths into block bi, newest first, covering `need`
-        wait states; one list per path"""
+        wait states (each instruction priced by `cost`); one list per path. A block already on the
+        path ends it (a loop is walked once around)."""
         if need <= 0 or bi in seen:
             return [[]]
         seen = seen | {bi}
@@ -58,7 +82,7 @@ def check(path, name, verbose=True):
         acc, w = [], 0
         for item in reversed(ins):
             acc.append(item)
-            w += (int(item[2]) + 1) if item[1] == "s_nop" and item[2].isdigit() else 1
+            w += cost(item)
             if w >= need:
                 return [acc]
         paths = []
@@ -66,7 +90,7 @@ def check(path, name, verbose=True):
             if p is None:
                 paths.append(acc)
             else:
-                for t in tail(p, need - w, seen):
+                for t in tail(p, need - w, seen, cost):
                     paths.append(acc + t)
         return paths
 
@@ -98,7 +122,7 @@ def check(path, name, verbose=True):
                     if ws >= WAIT_STATES:
                         break
                     if pop.startswith("v_") and not pop.startswith("v_mfma"):
-                        dst = regs(operands(prest)[0]) if prest else frozenset()
+                        dst = valu_dst(pop, prest)
                         if dst & srcs:
                             bad.setdefault(ln, f"line {ln + 1}: {op} reads {sorted(dst & srcs)[:4]} written by "
                                                f"{pop} at line {pl + 1}, {ws} wait states before")
@@ -106,23 +130,34 @@ def check(path, name, verbose=True):
     # MFMA write -> VALU access: the VALU must come >= XDL_WAIT wait states after an asm MFMA that
     # writes a register it reads or writes (19 covers the 16-pass case). An MFMA's own issue holds
     # its wave for >= 8 cycles (the microbenchmark's issue hold), so each one counts 8 here.
+    # The look-back walks every control-flow path into the VALU (tail()), so an MFMA before a
+    # branch or at the end of the previous loop iteration is seen as well.
     for bi, (_, ins, _) in enumerate(blocks):
         for k, (ln, op, rest) in enumerate(ins):
             if not op.startswith("v_") or op.startswith("v_mfma"):
                 continue
             used = regs(rest)
-            ws = 0
-            for pl, pop, prest in reversed(ins[:k]):
-                if ws >= XDL_WAIT:
+            acc, w = [], 0
+            for item in reversed(ins[:k]):
+                acc.append(item)
+                w += xdl_cost(item)
+                if w >= XDL_WAIT:
                     break
-                if pop.startswith("v_mfma"):
-                    dst = regs(operands(prest)[0])
-                    if dst & used:
-                        bad.setdefault(ln, f"line {ln + 1}: {op} touches {sorted(dst & used)[:4]} written by the MFMA "
-                                           f"at line {pl + 1}, {ws} wait states before")
-                    ws += 8
-                else:
-                    ws += (int(prest) + 1) if pop == "s_nop" and prest.isdigit() else 1
+            if w >= XDL_WAIT:
+                paths = [acc]
+            else:
+                paths = [acc + t for p in (preds[bi] or []) for t in tail(p, XDL_WAIT - w, frozenset(), xdl_cost)] or [acc]
+            for path in paths:
+                ws = 0
+                for pl, pop, prest in path:
+                    if ws >= XDL_WAIT:
+                        break
+                    if pop.startswith("v_mfma"):
+                        dst = regs(operands(prest)[0])
+                        if dst & used:
+                            bad.setdefault(ln, f"line {ln + 1}: {op} touches {sorted(dst & used)[:4]} written by the "
+                                               f"MFMA at line {pl + 1}, {ws} wait states before")
+                    ws += xdl_cost((pl, pop, prest))
     if verbose:
         for ln in sorted(bad)[:20]:
             print(bad[ln])

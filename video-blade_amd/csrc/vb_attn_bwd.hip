@@ -728,7 +728,8 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? VB_DQ_WAVES_D128 : V
       asm volatile("" : "+v"(df[s]));
     }
   }
-  const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
+  // the clamped row's statistics, as the Q/dO loads (padding rows are never stored)
+  const float* st = p.stats + ((int64_t)bh * p.ntile + gc / 64) * 256 + (gc & 63);
   float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];   // D1, D2 = -Delta
   asm volatile("" : "+v"(L1), "+v"(D1), "+v"(L2), "+v"(D2));
 

@@ -874,7 +874,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
   const bool qvalid = g < Lq;
   const int gc = qvalid ? g : Lq - 1;
   V8 qf[KS], df[KS];
-  const float* st = p.stats + ((int64_t)bh * p.ntile + g / 64) * 256 + (g & 63);
+  // row statistics of the clamped row, as the Q/dO loads (padding waves of a short last q-block
+  // would otherwise read past the stats region; their rows are never stored)
+  const float* st = p.stats + ((int64_t)bh * p.ntile + gc / 64) * 256 + (gc & 63);
   const float L1 = st[0], D1 = st[64], L2 = st[128], D2 = st[192];   // D1, D2 = -Delta
   {   // (these loads first: their latency overlaps the list build's mask loads)
     const uint8_t* qp = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + (qrow0 + gc) * p.qs[2]);
@@ -1204,9 +1206,16 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     }
 }
 
+// Kernel selection is read from the environment once per process (A/B switches), not per launch.
+static bool env_switch(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e ? atoi(e) : dflt) != 0;
+}
+
 bool dkdv_pipe_enabled(int D) {
-  const char* e = getenv(D == 128 ? "VB_BWD_KV128" : "VB_BWD_KV64");
-  return e ? atoi(e) != 0 : (D == 128 ? VB_BWD_KV128_DEFAULT : VB_BWD_KV64_DEFAULT) != 0;
+  static const bool on64 = env_switch("VB_BWD_KV64", VB_BWD_KV64_DEFAULT);
+  static const bool on128 = env_switch("VB_BWD_KV128", VB_BWD_KV128_DEFAULT);
+  return D == 128 ? on128 : on64;
 }
 
 template <int D>
@@ -1225,8 +1234,9 @@ static int launch_pipe(const BwdParams& p, bool pooled, bool f16, hipStream_t s)
 }
 
 bool dq_pipe_enabled(int D) {
-  const char* e = getenv(D == 128 ? "VB_BWD_DQ128" : "VB_BWD_DQ64");
-  return e ? atoi(e) != 0 : (D == 128 ? VB_BWD_DQ128_DEFAULT : VB_BWD_DQ64_DEFAULT) != 0;
+  static const bool on64 = env_switch("VB_BWD_DQ64", VB_BWD_DQ64_DEFAULT);
+  static const bool on128 = env_switch("VB_BWD_DQ128", VB_BWD_DQ128_DEFAULT);
+  return D == 128 ? on128 : on64;
 }
 
 template <int D>

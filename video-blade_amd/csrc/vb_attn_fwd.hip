@@ -984,18 +984,6 @@ static int dispatch_fwd(const FwdParams& p, int D, int dtype, bool pool, hipStre
 
 static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
-// vb_attn_fwd1.hip: the one-wave-per-SIMD inference kernel; sets `launched` when it covers the call
-int launch_fwd1(const FwdParams& p, int D, int dtype, bool pool, hipStream_t stream, bool& launched);
-#ifndef VB_FWD1_DEFAULT
-#define VB_FWD1_DEFAULT 0
-#endif
-static bool fwd1_enabled() {   // VB_FWD1=0 in the environment selects attn_fwd_kernel (A/B)
-  static const int on = [] {
-    const char* e = getenv("VB_FWD1");
-    return e ? atoi(e) : VB_FWD1_DEFAULT;
-  }();
-  return on != 0;
-}
 
 }  // namespace vb
 
@@ -1060,11 +1048,6 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_ATTN")) p.dbg = atoi(d);
 #endif
-  if (fwd1_enabled() && (a->D == 64 || a->D == 128)) {
-    bool launched = false;
-    const int rc = launch_fwd1(p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream), launched);
-    if (launched) return rc;
-  }
   return dispatch_fwd(p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream));
 }
 

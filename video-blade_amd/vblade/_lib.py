@@ -175,7 +175,11 @@ _lib = None
 
 
 class VBladeError(RuntimeError):
-    pass
+    """A failed library call; ``code`` is the VB_ERR_* value it returned (None for host checks)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 def load() -> ctypes.CDLL:
@@ -201,4 +205,4 @@ def load() -> ctypes.CDLL:
 def check(code: int, what: str):
     if code != VB_OK:
         msg = load().vb_last_error().decode(errors="replace")
-        raise VBladeError(f"{what} failed ({code}): {msg}")
+        raise VBladeError(f"{what} failed ({code}): {msg}", code)

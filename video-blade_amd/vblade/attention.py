@@ -161,10 +161,9 @@ class AdaptiveBlockSparseAttn(nn.Module):
         self.overlap = bool(cfg.get("overlap", True))
         # The attention kernel gathers K/V rows through the Gilbert index (True) or streams the
         # Gilbert-ordered contiguous copies the pooled pass writes (False: 2·L·D·2 bytes more per
-        # head, written beside the predictor). "auto" (default): copies whenever the one-wave-per-SIMD
-        # forward runs (it takes only them); with VB_FWD1=0 what measured faster per head dim for
-        # attn_fwd_kernel (tools/diag/overlap_ab.py --opt gather_kv): gather at D=128 (Wan, +2.4 % per
-        # call), copies at D=64 (CogVideoX, +0.9 %).
+        # head, written beside the predictor). "auto" (default): what measured faster per head dim
+        # (tools/diag/overlap_ab.py --opt gather_kv): gather at D=128 (Wan, +2.4 % per call), copies at
+        # D=64 (CogVideoX, +0.9 %).
         self.gather_kv = cfg.get("gather_kv", "auto")
 
     # -------------------------------------------------------------------------------- helpers
@@ -180,8 +179,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
     def _gather(self, D: int) -> bool:
         if self.gather_kv != "auto":
             return bool(self.gather_kv)
-        # the one-wave-per-SIMD forward (vb_attn_fwd1.hip) streams contiguous copies only
-        return D == 128 and not ops.FWD1
+        return D == 128
 
     def _count_slot(self, device):
         if self._kept_slots is None or self._kept_slots.device != device:

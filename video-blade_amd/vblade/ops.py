@@ -320,8 +320,14 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
                              min_keep=min_keep, max_keep=max_keep, force_tail=force_tail, scale=scale,
                              mask_count=mask_count, want_mask=want_mask, staged_event=staged_event,
                              rand=rand, philox=philox, pool=pool, pyr=pyr, level=level)
-    except Exception:
-        if philox is not None:   # the claimed draws were not used: give them back to the generator
+    except Exception as e:
+        # the claimed draws go back to the generator only when nothing was launched: a Python-side
+        # validation error, or the library refusing the call (VB_ERR_INVALID / _UNSUPPORTED, raised
+        # before any launch). After a VB_ERR_LAUNCH the sampling launch may already have consumed
+        # them, and rewinding would make the next torch.rand repeat those Philox values.
+        launched = isinstance(e, _lib.VBladeError) and e.code not in (_lib.VB_ERR_INVALID,
+                                                                      _lib.VB_ERR_UNSUPPORTED)
+        if philox is not None and not launched:
             release_rand_draws(q.device, philox)
         raise
 
@@ -411,9 +417,6 @@ def _mask_predict(q, k, q_off, k_off, *, rows, energy_threshold, min_keep, max_k
 # generator's Philox offset by 4.
 RAND_ONE_PASS_NUMEL = 524288   # the MI355X value; rand_one_pass_numel(device) is the per-device bound
 PHILOX_DRAWS = os.environ.get("VB_PHILOX_DRAWS", "1") != "0"   # off: the callers use torch.rand
-# VB_FWD1=1 selects the one-wave-per-SIMD inference forward (vb_attn_fwd1.hip) in the library and
-# the K/V source it needs here (the library reads the same variable; default: attn_fwd_kernel)
-FWD1 = os.environ.get("VB_FWD1", "0") != "0"
 _ONE_PASS = {}
 
 
