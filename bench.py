@@ -389,7 +389,8 @@ def run(args):
                             pt["traffic_detail"] = tr
             # the training path's backward of both TDM-trained variants (CogVideoX first: the
             # headline's model; Wan's sibling TDM script trains the D=128 geometry)
-            result["backward"] = [measure_backward("cog", dev), measure_backward("wan", dev)]
+            result["backward"] = [measure_backward("cog", dev), measure_backward("wan", dev),
+                                  measure_backward("cog-ml", dev)]
             result["end_to_end"] = measure_end_to_end(dev, ms_per_call, calls, frames)
         if world == 1 and not args.no_cpu_baseline:
             base = "cog" if args.variant == "cog-ml" else args.variant
@@ -591,16 +592,21 @@ def measure_backward(variant, dev, reps=6):
     through the mean pool) at the reference operating point, timed with HIP events around each
     launch; algorithmic FLOPs = 2.5 x the forward's (5 GEMMs per kept block pair against 2)."""
     import vblade
-    from vblade import ops
+    from vblade import multilevel, ops
     V = VARIANTS[variant]
     H, D = V["H"], V["D"]
-    mod = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+    ml = variant == "cog-ml"
+    if ml:   # the VBench sampler's multi-level op (vb_ml_attn_bwd), cogvideo_newattn.py:210-234
+        mod = multilevel.AdaptiveBlockSparseAttnTrain(log_every=0)
+    else:
+        mod = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
     L = mod.gilbert_rearranger.seq_len
-    Lkp = (L + mod.sample_gap - 1) // mod.sample_gap
+    Lkp = 0 if ml else (L + mod.sample_gap - 1) // mod.sample_gap
     q, k, v = (t.requires_grad_() for t in realistic_qkv(H, L, D, 700, dev))
     dout = torch.randn(1, H, L, D, device=dev, dtype=torch.bfloat16)
     events = []
-    orig = ops.attention_bwd
+    name = "ml_attention_bwd" if ml else "attention_bwd"
+    orig = getattr(ops, name)
 
     def timed(*a, **kw):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -610,23 +616,26 @@ def measure_backward(variant, dev, reps=6):
         events.append((e0, e1))
         return r
 
-    ops.attention_bwd = timed
+    setattr(ops, name, timed)
     flops = 0.0
     try:
         for i in range(reps + 2):
             out = mod(q, k, v)
             if i >= 2:
-                flops += attn_flops(mod.last_mask, L, D, Lkp)
+                flops += ml_attn_flops(mod.last_mask, L, D) if ml else attn_flops(mod.last_mask, L, D, Lkp)
             out.backward(dout)
             q.grad = k.grad = v.grad = None
         torch.cuda.synchronize()
     finally:
-        ops.attention_bwd = orig
+        setattr(ops, name, orig)
     ms = sum(a.elapsed_time(b) for a, b in events[2:]) / reps
     bflops = 2.5 * flops / reps
     tfs = bflops / (ms * 1e-3) / 1e12
-    return {"variant": variant, "kernel": "vb_attn_bwd (bwd_prep + bwd_dkdv + bwd_dq)",
-            "mask": "energy rule (reference defaults)", "avg_ms": round(ms, 4),
+    return {"variant": variant,
+            "kernel": ("vb_ml_attn_bwd (prep + pooled-level dK/dV + level-1 dK/dV + dQ)" if ml
+                       else "vb_attn_bwd (bwd_prep + bwd_dkdv + bwd_dq)"),
+            "mask": ("multi-level rank bands (reference mask_ratios)" if ml
+                     else "energy rule (reference defaults)"), "avg_ms": round(ms, 4),
             "flops_per_call": bflops, "achieved": round(tfs, 2), "unit": "TFLOP/s",
             "peak": PEAK_BF16_TFLOPS, "frac": round(tfs / PEAK_BF16_TFLOPS, 4),
             "launches_timed": reps,

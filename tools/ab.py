@@ -5,8 +5,9 @@ usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred
 TAG "cur" is the in-tree libvblade_hip.so; a "@torchrand" suffix runs that tag with the sampling
 draws made by torch.rand instead of inside the sampling launch (ops.PHILOX_DRAWS off), "@lvsep"
 with the multi-level mask as its own vb_level_mask launch (--what mlcall: the multi-level module),
-"@env:VAR=VAL+VAR=VAL" with those environment variables set around its launches (the library reads
-its VB_BWD_* switches per call)."""
+"@env:VAR=VAL+VAR=VAL" with those environment variables set around its launches. The library latches
+its VB_BWD_* kernel switches once per process (at its first backward call), so A/B a switch with a
+build variant instead (VB_EXTRA_FLAGS=-DVB_BWD_DQ128_DEFAULT=1 tools/build_variant.sh TAG)."""
 import argparse
 import ctypes
 import os
