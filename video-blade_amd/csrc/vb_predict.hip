@@ -117,6 +117,49 @@ struct PredParams {
 #ifndef VB_DIAG
 #define VB_DIAG 0
 #endif
+#ifndef VB_PRED_TRACE
+#define VB_PRED_TRACE 0   // diagnostic builds only (tools/diag/pred_trace.py): per-workgroup start/end times
+#endif
+#if VB_PRED_TRACE
+// [workgroup][start, end of waves 0-3, HW_ID, XCC_ID, kind, start and wave-0 end in shader cycles];
+// times in s_memrealtime ticks (100 MHz)
+constexpr int kTraceWgs = 4096;
+constexpr int kTraceF = 10;
+__device__ unsigned long long g_pred_trace[kTraceWgs][kTraceF];
+__device__ __forceinline__ unsigned long long trace_clk() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+__device__ __forceinline__ unsigned long long trace_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+__device__ __forceinline__ void trace_start(int kind) {
+  if (blockIdx.x < kTraceWgs && threadIdx.x == 0) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_pred_trace[blockIdx.x][0] = trace_now();
+    g_pred_trace[blockIdx.x][5] = hw;
+    g_pred_trace[blockIdx.x][6] = xcc;
+    g_pred_trace[blockIdx.x][7] = kind;
+    g_pred_trace[blockIdx.x][8] = trace_clk();
+  }
+}
+__device__ __forceinline__ void trace_end() {
+  if (blockIdx.x < kTraceWgs && (threadIdx.x & 63) == 0) {
+    g_pred_trace[blockIdx.x][1 + (threadIdx.x >> 6)] = trace_now();
+    if (threadIdx.x == 0) g_pred_trace[blockIdx.x][9] = trace_clk();
+  }
+}
+#define VB_TRACE_START(k) trace_start(k)
+#define VB_TRACE_END() trace_end()
+#else
+#define VB_TRACE_START(k)
+#define VB_TRACE_END()
+#endif
 #ifndef VB_PRED_STAMPS
 #define VB_PRED_STAMPS 0   // diagnostic builds only (tools/pred_stamps.py): per-phase s_memtime sums
 #endif
@@ -460,11 +503,14 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
   const int wg = (int)blockIdx.x;
 #else
   if ((int)blockIdx.x < p.n_pool) {
+    VB_TRACE_START(1);
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)p.n_pool * blockDim.x;
     if (p.pool_kind == 2) kv_pyramid_span<D, T>(p.pyr, i0, st);
     else pool_kv_span<T>(p.pool, i0, st);
+    VB_TRACE_END();
     return;
   }
+  VB_TRACE_START(0);
   const int wg = (int)blockIdx.x - p.n_pool;
 #endif
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -833,6 +879,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
 #pragma unroll
   for (int e = 0; e < KQ; ++e)
     if (qbs[e] < nb) epilogue(qbs[e], Rqs[e], mrow_s + (wave * KQ + e) * 32);
+  VB_TRACE_END();
 }
 
 // random_sample_tokens' topk (cogvideo_blocksparseattn.py:45-46): for every row of `n` uniform draws,
@@ -928,6 +975,15 @@ static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t st
 
 }  // namespace vb
 
+#if VB_PRED_TRACE
+// diagnostic builds only: read and clear the per-workgroup trace (n rows of kTraceF u64)
+extern "C" int vb_debug_pred_trace(unsigned long long* out, int n) {
+  const size_t bytes = sizeof(unsigned long long) * vb::kTraceF * (size_t)(n < vb::kTraceWgs ? n : vb::kTraceWgs);
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vb::g_pred_trace), bytes) != hipSuccess) return -1;
+  static unsigned long long z[vb::kTraceWgs][vb::kTraceF];
+  return hipMemcpyToSymbol(HIP_SYMBOL(vb::g_pred_trace), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 #if VB_PRED_STAMPS
 // diagnostic builds only: read and clear the score kernel's phase sums
 extern "C" int vb_debug_pred_stamps(unsigned long long* out) {
