@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-workgroup timeline of the predictor's launch (diagnostic build: VB_PRED_FLAGS=-DVB_PRED_TRACE=1
-tools/build_variant.sh ptrace): start and per-wave end times (s_memrealtime, 10 ns), CU and XCD of
-every workgroup. Prints how long score and pooling workgroups live, when they start, and how many
-are resident per CU over the launch (slot utilisation).
-usage: python tools/diag/pred_trace.py [cog|wan] [pred|call] [TAG]"""
+tools/build_variant.sh ptrace) or of the attention kernel's (what = attn; VB_EXTRA_FLAGS=-DVB_ATTN_TRACE=1
+tools/build_variant.sh atrace): start and per-wave end times (s_memrealtime, 10 ns), CU and XCD of
+every workgroup, and the shader clock over it. Prints how long the workgroups live, when they start,
+and how many are resident per CU over the launch (slot utilisation, the tail).
+usage: python tools/diag/pred_trace.py [cog|wan] [pred|call|attn] [TAG]"""
 import ctypes
 import os
 import sys
@@ -22,10 +23,11 @@ from bench import realistic_qkv  # noqa: E402
 
 variant = sys.argv[1] if len(sys.argv) > 1 else "cog"
 what = sys.argv[2] if len(sys.argv) > 2 else "pred"
-tag = sys.argv[3] if len(sys.argv) > 3 else "ptrace"
+tag = sys.argv[3] if len(sys.argv) > 3 else ("atrace" if what == "attn" else "ptrace")
 lib = ab.load(tag)
-lib.vb_debug_pred_trace.restype = ctypes.c_int
-lib.vb_debug_pred_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+getter = getattr(lib, "vb_debug_attn_trace" if what == "attn" else "vb_debug_pred_trace")
+getter.restype = ctypes.c_int
+getter.argtypes = [ctypes.c_void_p, ctypes.c_int]
 _lib._lib = lib
 dev = torch.device("cuda")
 H, D = (48, 64) if variant == "cog" else (12, 128)
@@ -34,17 +36,17 @@ L = m.gilbert_rearranger.seq_len
 q, k, v = realistic_qkv(H, L, D, 0, dev)
 qo = vblade.draw_sample_offsets(1, H, dev)
 ko = vblade.draw_sample_offsets(1, H, dev)
-N = 4096
+N = 8192
 F = 10
 buf = (ctypes.c_ulonglong * (F * N))()
 with torch.no_grad():
     for _ in range(5):
         m.predict_mask(q, k, qo, ko) if what == "pred" else m(q, k, v)
     torch.cuda.synchronize()
-    lib.vb_debug_pred_trace(buf, N)   # clear
+    getter(buf, N)   # clear
     m.predict_mask(q, k, qo, ko) if what == "pred" else m(q, k, v)
     torch.cuda.synchronize()
-    assert lib.vb_debug_pred_trace(buf, N) == 0
+    assert getter(buf, N) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(N, F).astype(np.int64)
 a = a[a[:, 0] > 0]
 t0 = a[:, 0].min()
@@ -56,7 +58,7 @@ wave_end = (ends - t0) / 100.0
 kind = a[:, 7]
 hw, xcc = a[:, 5], a[:, 6]
 cu = (xcc << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
-print(f"{variant} {what}: {len(a)} workgroups traced ({(kind == 1).sum()} pooling), launch span {end.max():.1f} us")
+print(f"{variant} {what}: {len(a)} workgroups traced ({(kind == 1).sum()} pooling), launch span {np.nanmax(end):.1f} us")
 for kd, name in ((0, "score"), (1, "pool")):
     s = kind == kd
     if not s.any():
@@ -71,10 +73,11 @@ for kd, name in ((0, "score"), (1, "pool")):
     ws = np.nanmax(wave_end[s], 1) - np.nanmin(wave_end[s], 1)
     print(f"         wave end spread within a workgroup p50/p90 {np.median(ws):5.1f} {np.percentile(ws, 90):5.1f} us")
 ncu = len(np.unique(cu))
+end = np.where(np.isnan(end), start, end)
 T = np.arange(0, end.max(), 1.0)
 res = np.array([((start <= t) & (end > t)).sum() for t in T]) / ncu
 print(f"  {ncu} CUs; resident workgroups per CU over time (1 us bins, every 10th):")
-print("   " + " ".join(f"{x:.1f}" for x in res[::10]))
+print("   " + " ".join(f"{x:.1f}" for x in res[::max(1, len(res) // 40)]))
 print(f"  mean residency {res.mean():.2f} per CU; score-only residency "
       f"{np.mean([((start <= t) & (end > t) & (kind == 0)).sum() for t in T]) / ncu:.2f}")
 per_cu = np.bincount(np.unique(cu, return_inverse=True)[1])

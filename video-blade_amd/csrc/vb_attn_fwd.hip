@@ -23,6 +23,19 @@
 #include <type_traits>
 
 #include "vb_attn_fwd.hpp"
+#include "vb_trace.hpp"
+
+#ifndef VB_ATTN_TRACE
+#define VB_ATTN_TRACE 0   // diagnostic builds only (tools/diag/attn_trace.py): per-workgroup timeline
+#endif
+#if VB_ATTN_TRACE
+namespace vb { __device__ TraceBuf g_attn_trace; }
+#define VB_ATRACE_START(k) trace_start(g_attn_trace, k)
+#define VB_ATRACE_END() trace_end(g_attn_trace)
+#else
+#define VB_ATRACE_START(k)
+#define VB_ATRACE_END()
+#endif
 
 namespace vb {
 
@@ -96,6 +109,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   //  phase 2: every XCD takes a contiguous, head-major range of the remaining (head, q-block)
   //           work, so the pooled K/V and the kept K/V blocks of the one or two heads an XCD is
   //           working on are re-read from its own L2 instead of the Infinity Cache / HBM.
+  VB_ATRACE_START(0);
   const int BH = p.B * p.H;
   const int hr = min(p.heavy_rows, p.nbq);
   const int n_heavy = hr * BH;
@@ -943,6 +957,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       else *dst = (p.cu_q && !(lt > 0.f)) ? INFINITY : v;
     }
   }
+  VB_ATRACE_END();
 }
 
 template <int D, class T>
@@ -1050,6 +1065,10 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
 #endif
   return dispatch_fwd(p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream));
 }
+
+#if VB_ATTN_TRACE
+VB_TRACE_GETTER(vb_debug_attn_trace, vb::g_attn_trace)
+#endif
 
 extern "C" int vb_kv_pyramid_rows(int L) {
   const int lpad = (L + vb::kQBlk - 1) / vb::kQBlk * vb::kQBlk;

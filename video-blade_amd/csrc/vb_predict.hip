@@ -21,6 +21,7 @@
 #include "vb_tiles.hpp"
 #include "vb_pool.hpp"
 #include "vb_pyr.hpp"
+#include "vb_trace.hpp"
 
 namespace vb {
 
@@ -121,41 +122,9 @@ struct PredParams {
 #define VB_PRED_TRACE 0   // diagnostic builds only (tools/diag/pred_trace.py): per-workgroup start/end times
 #endif
 #if VB_PRED_TRACE
-// [workgroup][start, end of waves 0-3, HW_ID, XCC_ID, kind, start and wave-0 end in shader cycles];
-// times in s_memrealtime ticks (100 MHz)
-constexpr int kTraceWgs = 4096;
-constexpr int kTraceF = 10;
-__device__ unsigned long long g_pred_trace[kTraceWgs][kTraceF];
-__device__ __forceinline__ unsigned long long trace_clk() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-__device__ __forceinline__ unsigned long long trace_now() {
-  unsigned long long t;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-__device__ __forceinline__ void trace_start(int kind) {
-  if (blockIdx.x < kTraceWgs && threadIdx.x == 0) {
-    unsigned hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_pred_trace[blockIdx.x][0] = trace_now();
-    g_pred_trace[blockIdx.x][5] = hw;
-    g_pred_trace[blockIdx.x][6] = xcc;
-    g_pred_trace[blockIdx.x][7] = kind;
-    g_pred_trace[blockIdx.x][8] = trace_clk();
-  }
-}
-__device__ __forceinline__ void trace_end() {
-  if (blockIdx.x < kTraceWgs && (threadIdx.x & 63) == 0) {
-    g_pred_trace[blockIdx.x][1 + (threadIdx.x >> 6)] = trace_now();
-    if (threadIdx.x == 0) g_pred_trace[blockIdx.x][9] = trace_clk();
-  }
-}
-#define VB_TRACE_START(k) trace_start(k)
-#define VB_TRACE_END() trace_end()
+__device__ TraceBuf g_pred_trace;
+#define VB_TRACE_START(k) trace_start(g_pred_trace, k)
+#define VB_TRACE_END() trace_end(g_pred_trace)
 #else
 #define VB_TRACE_START(k)
 #define VB_TRACE_END()
@@ -666,6 +635,12 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
 #if VB_PRED_STAMPS
   unsigned long long pst[4] = {0, 0, 0, 0};
 #endif
+  auto halfmax = [&](const f32x16& a) __attribute__((always_inline)) -> float {
+    float y = fmaxf(fmaxf(a[0], a[1]), a[2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) y = fmaxf(fmaxf(y, a[r]), a[r + 1]);
+    return fmaxf(y, a[15]);
+  };
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
     VB_PST(b0);
@@ -740,38 +715,32 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     // row maxima, two 32-key blocks per v_permlane32_swap: after the swap lanes 0-31 hold block
     // 2pr's full row max and lanes 32-63 block 2pr+1's (the halves of each block's C tile meet)
     const int j0 = kKT * t;
+    constexpr int kPairs = kKT / 2;
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
     float mxp[kKT / 2];
 #pragma unroll
-    for (int pr = 0; pr < kKT / 2; ++pr) {
-      float x[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const f32x16& a = sc[q][2 * pr + e];
-        float y = fmaxf(fmaxf(a[0], a[1]), a[2]);
-#pragma unroll
-        for (int r = 3; r < 15; r += 2) y = fmaxf(fmaxf(y, a[r]), a[r + 1]);
-        x[e] = fmaxf(y, a[15]);
-      }
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]), __float_as_uint(x[1]), false, false);
+    for (int pr = 0; pr < kPairs; ++pr) {
+      const float x0 = halfmax(sc[q][2 * pr]), x1 = halfmax(sc[q][2 * pr + 1]);
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
       mxp[pr] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * p.c;   // tl.max(qk, 1) * qk_scale
     }
     if (j0 + kKT > nb) {   // partial last tile: blocks past nb take no part (their rows are zeros)
       asm volatile("");
 #pragma unroll
-      for (int pr = 0; pr < kKT / 2; ++pr)
+      for (int pr = 0; pr < kPairs; ++pr)
         if (j0 + 2 * pr + half >= nb) mxp[pr] = -INFINITY;
     }
 #pragma unroll
-    for (int pr = 0; pr < kKT / 2; ++pr) m[q] = fmaxf(m[q], mxp[pr]);   // this half's blocks; halves meet below
+    for (int pr = 0; pr < kPairs; ++pr) m[q] = fmaxf(m[q], mxp[pr]);   // this half's blocks; halves meet below
     // R[j][row]: lane (half, row) stores block j0 + 2pr + half, so one store writes 128 contiguous
     // bytes. Issued unconditionally (kSt per body, the vmcnt arithmetic above relies on it): blocks
     // past nb fall outside the descriptor and an inactive q-block's descriptor is empty, so the
     // hardware drops those lanes.
 #pragma unroll
-    for (int pr = 0; pr < kKT / 2; ++pr) store16(rsrd[q], (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
+    for (int pr = 0; pr < kPairs; ++pr) store16(rsrd[q], (uint16_t)storage_bits<T>(mxp[pr]), lane * 2, (j0 + 2 * pr) * 64);
     }
+
 #if VB_PRED_STAMPS
     VB_PST(b4);
     pst[3] += b4 - b0;
@@ -786,6 +755,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
       if (t0 + 3 < ntiles) body(t0 + 3, std::integral_constant<int, 3>{});
   }
   static_assert(kBufs >= 2 && kBufs <= 4, "the loop body is instantiated once per ring slot");
+
 #if VB_PRED_GATHER
   VB_WAIT_VMCNT(0);   // the DMAs issued past the last tile land before the epilogue reuses the LDS
 #endif
@@ -976,13 +946,7 @@ static int launch_predict(const PredParams& p, hipStream_t stream, hipEvent_t st
 }  // namespace vb
 
 #if VB_PRED_TRACE
-// diagnostic builds only: read and clear the per-workgroup trace (n rows of kTraceF u64)
-extern "C" int vb_debug_pred_trace(unsigned long long* out, int n) {
-  const size_t bytes = sizeof(unsigned long long) * vb::kTraceF * (size_t)(n < vb::kTraceWgs ? n : vb::kTraceWgs);
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vb::g_pred_trace), bytes) != hipSuccess) return -1;
-  static unsigned long long z[vb::kTraceWgs][vb::kTraceF];
-  return hipMemcpyToSymbol(HIP_SYMBOL(vb::g_pred_trace), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
+VB_TRACE_GETTER(vb_debug_pred_trace, vb::g_pred_trace)
 #endif
 #if VB_PRED_STAMPS
 // diagnostic builds only: read and clear the score kernel's phase sums
