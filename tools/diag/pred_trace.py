@@ -49,6 +49,9 @@ with torch.no_grad():
     assert getter(buf, N) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(N, F).astype(np.int64)
 a = a[a[:, 0] > 0]
+out = os.environ.get("TRACE_OUT")
+if out:   # the raw rows, for offline analysis
+    np.save(out, a)
 t0 = a[:, 0].min()
 start = (a[:, 0] - t0) / 100.0          # us
 ends = a[:, 1:5].astype(np.float64)
@@ -82,3 +85,14 @@ print(f"  mean residency {res.mean():.2f} per CU; score-only residency "
       f"{np.mean([((start <= t) & (end > t) & (kind == 0)).sum() for t in T]) / ncu:.2f}")
 per_cu = np.bincount(np.unique(cu, return_inverse=True)[1])
 print(f"  workgroups per CU min/median/max {per_cu.min()} {int(np.median(per_cu))} {per_cu.max()}")
+# duration against the residency of the workgroup's CU while it ran (is a workgroup faster alone?)
+cu_id = np.unique(cu, return_inverse=True)[1]
+occ = np.zeros(len(a))
+for i in range(len(a)):
+    same = (cu_id == cu_id[i]) & (start < end[i]) & (end > start[i])
+    occ[i] = same.sum()
+dur = end - start
+for lo, hi in ((1, 1.5), (1.5, 2.5), (2.5, 3.5), (3.5, 9)):
+    s_ = (occ >= lo) & (occ < hi) & (kind == 0)
+    if s_.any():
+        print(f"  co-resident workgroups on its CU {lo:.1f}-{hi:.1f}: {s_.sum():5d} workgroups, duration p50 {np.median(dur[s_]):6.1f} us")

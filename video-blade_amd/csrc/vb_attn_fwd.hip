@@ -428,7 +428,9 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     const int rowb = pooled ? my_prowb : my_rowb;
     const int soff = __builtin_amdgcn_readfirstlane(src.kstart * rowb);
     if (src.klen == kKT) {
-      const int vb0 = my_row0 * rowb;
+      // 24-bit multiply (full rate; v_mul_lo_u32 is a quarter-rate op on every tile): the row is
+      // < 64 and the host rejects row strides of 2^24 bytes or more
+      const int vb0 = (int)__umul24((unsigned)my_row0, (unsigned)rowb);
 #pragma unroll
       for (int i = 0; i < kInstPerWave; ++i)
         piece(i, pooled ? my_prsrc : my_rsrc, vb0 + my_rc[i], __builtin_amdgcn_readfirstlane(soff + i * kRowsPerInst * rowb));
@@ -486,14 +488,16 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
                  v_off_bytes<D>(vrow, dt * 32 + vcol);
 
   // One 64-key tile in ring slot U: S^T = K.Q^T, online softmax, O^T += V^T.P^T.
-  auto tile_step = [&](auto U, float bias, int klen) __attribute__((always_inline)) {
+  // bias_bits: the tile's logit bias (exp2 domain) as a bit pattern, chosen by the caller with scalar
+  // selects (a float select would be a v_cndmask + v_readfirstlane on every tile)
+  auto tile_step = [&](auto U, int bias_bits, int klen) __attribute__((always_inline)) {
     constexpr int kSlot = decltype(U)::value;
     const uint8_t* kl = smem + kSlot * kBufBytes;
+    const float bias = __int_as_float(bias_bits);
     f32x16 s[2];
     if constexpr (kCBias) {
       // wave-uniform; only where the tile source changes (pooled, levels). Compared as bit patterns
       // in SGPRs (a scalar compare; a float compare would run on the VALU every tile)
-      const int bias_bits = __builtin_amdgcn_readfirstlane(__float_as_int(bias));
       if (bias_bits != cur_bias_bits) {
         asm volatile("");
         const float db = bias - __int_as_float(cur_bias_bits);
@@ -828,6 +832,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     else issue(src, slot);
   };
   Src slot_src[kBufs];
+  const int pool_bias_bits = __builtin_amdgcn_readfirstlane(__float_as_int(p.pool_bias_l2));
   int next_blk, idx_blk = 0;
   if constexpr (kKvRows) {
     // I0 .. I(kBufs-1), then the rows of tiles 0 .. kBufs-2, each once its offsets have landed
@@ -895,11 +900,15 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     VB_STAMP(st2);
     VB_ACC(1, st2 - st1);
     const Src src = slot_src[u];
-    float bias;
-    if constexpr (kML) bias = (float)src.lvl;   // + ln(p) in the exp2 domain: log2(p)
-    else bias = (kPool && src.pooled) ? p.pool_bias_l2 : 0.f;
+    int bias_bits;
+    if constexpr (kML) {   // + ln(p) in the exp2 domain: log2(p) in {0, 1, 2, 3}
+      bias_bits = src.lvl == 0 ? 0 : src.lvl == 1 ? 0x3F800000 : src.lvl == 2 ? 0x40000000 : 0x40400000;
+    } else {
+      bias_bits = (kPool && src.pooled) ? pool_bias_bits : 0;
+    }
+    bias_bits = __builtin_amdgcn_readfirstlane(bias_bits);
     if (VB_DIAG && (p.dbg & 2)) return;   // diagnostic: stream tiles only
-    tile_step(U, bias, src.klen);
+    tile_step(U, bias_bits, src.klen);
     VB_STAMP(st3);
     VB_ACC(2, st3 - st2);
   };
@@ -1032,8 +1041,12 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
     if (a->use_main && ((a->k_stride[i] | a->v_stride[i]) & 7)) return fail(VB_ERR_INVALID, "vb_attn_fwd: k/v strides must be multiples of 8 elements");
     if (pool && ((a->kp_stride[i] | a->vp_stride[i]) & 7)) return fail(VB_ERR_INVALID, "vb_attn_fwd: kp/vp strides must be multiples of 8 elements");
   }
-  if (a->kv_rows && (a->Lk >= (1 << 24) || a->k_stride[2] * 2 >= (1 << 24) || a->v_stride[2] * 2 >= (1 << 24)))
-    return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: kv_rows needs Lk and the k/v row strides (bytes) < 2^24");
+  if (a->kv_rows && a->Lk >= (1 << 24))
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: kv_rows needs Lk < 2^24");
+  // the tile DMA offsets use 24-bit multiplies: row strides below 2^24 bytes (16 MiB per row)
+  if ((a->use_main && (a->k_stride[2] * 2 >= (1 << 24) || a->v_stride[2] * 2 >= (1 << 24))) ||
+      (pool && (a->kp_stride[2] * 2 >= (1 << 24) || a->vp_stride[2] * 2 >= (1 << 24))))
+    return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: k/v/kp/vp row strides must be < 2^24 bytes");
   const int64_t kLim = int64_t(1) << 31;   // one (b,h) slice must be addressable by a 32-bit buffer offset
   if (a->use_main && ((int64_t)(a->Lk - 1) * 2 * (a->k_stride[2] > a->v_stride[2] ? a->k_stride[2] : a->v_stride[2]) + 2 * a->D >= kLim))
     return fail(VB_ERR_UNSUPPORTED, "vb_attn_fwd: a k/v (b,h) slice spans >= 2 GiB");
