@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VB_ABI_VERSION 2   /* 2: mask_head_mode argument of vb_block_sparse_attn_fwd/bwd */
+#define VB_ABI_VERSION 3   /* 2: mask_head_mode argument of vb_block_sparse_attn_fwd/bwd; 3: vb_attn_args.q_order */
 
 enum vb_status {
   VB_OK = 0,
@@ -107,6 +107,15 @@ typedef struct vb_attn_args {
   int dtype;
   int heavy_rows;         /* scheduling hint: the last N q-block rows keep (almost) every key
                              block (CogVideoX's forced text rows: 2); 0 = none. Never affects results. */
+  int32_t* q_order;       /* scheduling workspace [B*H*ceil(Lq/128)] int32, or NULL (ABI 3): with a
+                             block mask, each XCD's q-blocks are dispatched head by head, longest
+                             (most kept key blocks) first, so its last workgroups are the short ones.
+                             Written by a small launch before the attention kernel. Never affects results. */
+  const int32_t* q_lengths; /* [B,H,ceil(Lq/128)] kept key blocks per mask row (vb_predict_args.
+                             mask_rows_kept), or NULL: the ordering launch counts them from the mask */
+  int order_window;       /* > 0: only the last order_window q-blocks of each XCD range are re-ordered
+                             (the tail; the rest keeps the kernel's head-major, Gilbert-neighbour
+                             order and its L2 reuse); 0: the whole range */
 } vb_attn_args;
 int vb_attn_fwd(const vb_attn_args* args, void* stream);
 
@@ -182,6 +191,9 @@ typedef struct vb_predict_args {
   const int32_t* level_band_value;
   const double* level_band_start;
   const double* level_band_end;
+  /* mask_rows_kept (ABI 3, nullable): [B,H,nb] int32, the number of key blocks the energy rule kept
+   * in each mask row (the attention kernel's per-q-block work, for vb_attn_args.q_lengths). */
+  int32_t* mask_rows_kept;
 } vb_predict_args;
 uint64_t vb_mask_predict_workspace_size(const vb_predict_args* args);
 int vb_mask_predict(const vb_predict_args* args, void* stream);

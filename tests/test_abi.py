@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.vb_abi_version() == 2
+    assert lib.vb_abi_version() == 3
 
 
 def test_struct_layouts_match_header():

@@ -330,6 +330,41 @@ def test_forward_is_bitwise_deterministic_at_full_size(variant, H, D):
         assert torch.equal(o, outs[0])
 
 
+@pytest.mark.parametrize("variant,H,D", [("cog", 48, 64), ("wan", 12, 128)])
+def test_longest_first_dispatch_order_is_bit_identical(variant, H, D):
+    """Round 5 scheduling: with ``order`` the attention launch dispatches each XCD's q-blocks head by
+    head, most kept key blocks first (vb_attn_args.q_order; lengths from the predictor's
+    mask_rows_kept or counted on the device). Outputs must equal the kernel's own order bit for
+    bit, and the predictor's kept counts must equal the mask rows' counts."""
+    import vblade
+    from vblade import ops
+    m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+    L = m.gilbert_rearranger.seq_len
+    g = torch.Generator(device=DEV).manual_seed(5)
+    q, k, v = (torch.randn(1, H, L, D, generator=g, device=DEV).to(torch.bfloat16) for _ in range(3))
+    offs = torch.zeros(1, H, 32, dtype=torch.int32, device=DEV) + torch.arange(32, dtype=torch.int32, device=DEV)
+    with torch.no_grad():
+        m.order = False
+        ref = m(q, k, v, q_off=offs, k_off=offs)
+        m.order = True
+        got = m(q, k, v, q_off=offs, k_off=offs)
+        assert torch.equal(got, ref)
+        # the predictor's kept counts are the mask rows' counts
+        nb = (L + 127) // 128
+        kept = torch.full((1, H, nb), -1, dtype=torch.int32, device=DEV)
+        _, mask = m.predict_mask(q, k, offs, offs, rows_kept=kept)
+        assert torch.equal(kept, (mask != 0).sum(-1).to(torch.int32))
+        # the op level: lengths counted on the device, and given
+        rows = m._rows(q.device)
+        kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
+        kw = dict(block_mask=mask, q_rows=rows, kp=kp, vp=vp, kp_log_bias=m._log_gap(q.dtype),
+                  heavy_rows=m.force_tail)
+        a = ops.attention_fwd(q, k_r, v_r, **kw)
+        b = ops.attention_fwd(q, k_r, v_r, order=True, **kw)
+        c = ops.attention_fwd(q, k_r, v_r, order=True, q_lengths=kept, **kw)
+        assert torch.equal(a, b) and torch.equal(a, c)
+
+
 def test_sample_offsets_match_torch_topk_and_rng_order():
     """vb_sample_offsets == torch.topk(rand, 32).indices (the reference's random_sample_tokens,
     :45-46), and the module draws q then k from the same generator stream as the reference."""

@@ -5,6 +5,8 @@ usage: python tools/ab.py TAG_A TAG_B [--variant cog|wan|both] [--what attn|pred
 TAG "cur" is the in-tree libvblade_hip.so; a "@torchrand" suffix runs that tag with the sampling
 draws made by torch.rand instead of inside the sampling launch (ops.PHILOX_DRAWS off), "@lvsep"
 with the multi-level mask as its own vb_level_mask launch (--what mlcall: the multi-level module),
+"@noorder" with the attention launches in the kernel's own q-block order (no longest-first sort),
+"@win:N" with only the last N q-blocks of each XCD range re-ordered,
 "@env:VAR=VAL+VAR=VAL" with those environment variables set around its launches. The library latches
 its VB_BWD_* kernel switches once per process (at its first backward call), so A/B a switch with a
 build variant instead (VB_EXTRA_FLAGS=-DVB_BWD_DQ128_DEFAULT=1 tools/build_variant.sh TAG)."""
@@ -40,9 +42,17 @@ def load(tag):
     return lib
 
 
+ORDER = [True, 0]
+
+
 def select(tag, libs):
     """make `tag` the active variant: its library, its module switches and its environment"""
     _lib._lib = libs[tag]
+    ORDER[0] = "@noorder" not in tag
+    ORDER[1] = 0
+    for part in tag.split("@")[1:]:
+        if part.startswith("win:"):
+            ORDER[1] = int(part[4:])
     ops.PHILOX_DRAWS = "@torchrand" not in tag
     multilevel.FUSED_LEVEL_MASK = "@lvsep" not in tag
     for kv in ENV_SET:
@@ -81,10 +91,12 @@ def main():
         _, mask = m.predict_mask(q, k, qo, ko)
         kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
         fl = attn_flops(mask, L, D, kp.shape[2])
+        qlen = (mask != 0).sum(-1).to(torch.int32).contiguous()
         if a.what == "attn":
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp,  # noqa
                                            vp=vp, kp_log_bias=m._log_gap(q.dtype),
-                                           heavy_rows=m.force_tail)
+                                           heavy_rows=m.force_tail, order=ORDER[0], q_lengths=qlen,
+                                           order_window=ORDER[1])
         elif a.what == "fwdlse":   # the training forward's main branch (LSE out: the non-lazy kernel)
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,  # noqa
                                            heavy_rows=m.force_tail)[0]
@@ -114,7 +126,9 @@ def main():
             mlm = multilevel.AdaptiveBlockSparseAttnTrain(log_every=0)
             fn = lambda: mlm(q, k, v)  # noqa
         else:
-            fn = lambda: m(q, k, v)  # noqa
+            def fn():
+                m.order, m.order_window = ORDER[0], ORDER[1]
+                return m(q, k, v)
         ref = None
         times = {kk: [] for kk in keys}
         with torch.no_grad():

@@ -1,0 +1,7 @@
+set -o pipefail
+O=gpurun_out/r05_c11
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_forward.py -x -q --timeout 120 --timeout-method thread -k "longest_first or deterministic or block_mask or fused_pooled" > $O/pytest.log 2>&1 && \
+timeout -k 10 300 python tools/ab.py cur@noorder cur cur@noorder cur --what attn --variant both > $O/attn.log 2>&1 && \
+timeout -k 10 300 python tools/ab.py cur@noorder cur --what call --variant both > $O/call.log 2>&1
+rc=$?; tail -3 $O/pytest.log; grep -h -E "median|identical" $O/attn.log $O/call.log; exit $rc

@@ -36,6 +36,12 @@
 #ifndef VB_BWD_DQ128_DEFAULT
 #define VB_BWD_DQ128_DEFAULT 0
 #endif
+#ifndef VB_BWD_DQ128_RING
+#define VB_BWD_DQ128_RING 4  // ring slots of the D=128 dQ pipeline: 4, or 2 (two workgroups per CU)
+#endif
+#ifndef VB_DQ2_LA
+#define VB_DQ2_LA 2        // operand lookahead of the 2-slot dQ pipeline
+#endif
 #ifndef VB_BWD_DQ64_DEFAULT
 #define VB_BWD_DQ64_DEFAULT 1
 #endif
@@ -264,41 +270,71 @@ __device__ __forceinline__ void vgap(f32x16& s, f32x16& dp, const f32x4 (&lq)[4]
 // ---- the dQ kernel's schedule (bwd_dq_pipe_kernel): per 64-key tile t, sections
 //   A = X(t,0) S^T = K.Q^T, dP^T = V.dO^T of keys 0-31 (kX MFMAs)   B = Y(t-1,1) dQ^T of keys 32-63 (kY)
 //   C = X(t,1) keys 32-63                                          D = Y(t,0)   keys 0-31
-template <int D>
+// R = 4: a 4-slot K/V ring, one barrier per tile (kGb), the DMA of tile t+3 after it.
+// R = 2: a 2-slot ring (64 KiB at D=128, so two workgroups per CU) filled half a tile at a time,
+// with two barriers per tile. Half h of a tile is read by X(t,h) and, for K, by Y(t,h) one section
+// (h = 0) or two (h = 1) later; each barrier first drains the wave's LDS reads, so the halves whose
+// last reads precede it are free:
+//   G1 = kC - L (before C's first operand reads): K half 1 of t-1 and V half 0 of t are free, and
+//       half 1 of t must have landed; then the DMA of half 1 of tile t+1 (into t-1's slot);
+//   G2 = N - L (before tile t+1's first reads): K half 0 and V half 1 of t are free, half 0 of t+1
+//       must have landed; the DMA of half 0 of tile t+2 (into t's slot) follows in gaps 0.. of t+1.
+// Every barrier waits for all but the last half-tile batch (vmcnt = kPieces / 2); each batch is
+// issued a whole tile (N - L gaps or more) before its barrier.
+template <int D, int R = 4, int L = kLA>
 struct QSched {
+  static_assert(R == 2 || R == 4, "ring slots");
+  static_assert(L >= 2 && L <= 4, "lookahead");
   static constexpr int KS = D / 16, DT = D / 32, RB = 2 * D;
   static constexpr int kTileBytes = bwd::kT * RB;
+  static constexpr int LA = L;
   static constexpr int kX = 2 * KS, kY = 2 * DT;
   static constexpr int N = 2 * kX + 2 * kY;
   static constexpr int kB = kX, kC = kX + kY, kD = 2 * kX + kY;
   static constexpr int kKOff = 0;
-  static constexpr int kVOff = 4 * kTileBytes;
-  static constexpr int kListOff = 8 * kTileBytes;
+  static constexpr int kVOff = R * kTileBytes;
+  static constexpr int kListOff = 2 * R * kTileBytes;
   static constexpr int kLdsBytes = kListOff + 2 * bwd::kMaxBlocks + 16 + 4 * (bwd::kMaxBlocks / 64);
   static constexpr int kPQ = kTileBytes / 1024 / 4;
   static constexpr int kPieces = 2 * kPQ;
   static constexpr int kRpp = 1024 / RB;
   static constexpr int kV0 = kB + 2, kV0n = kD - kV0;          // V(t,0): [kB+2, kD)
   static constexpr int kV1 = kD + 2, kV1n = N - kV1 + kB;      // V(t,1): [kD+2, N) and [0, kB) of t+1
-  static constexpr int kGb = N - 12;                           // the tile barrier (after section B)
-  static constexpr int kList = kGb - 6;                        // the key block of tile t+3
-  static constexpr int kNx = kGb + 1;                          // tile t+1's first operands
+  // R = 4
+  static constexpr int kGb = R == 4 ? N - 12 : -1;             // the tile barrier (after section B)
   static constexpr int kDma0 = kGb + 1;
-  static_assert(kGb >= kC, "the barrier must follow the reads of the previous tile");
-  static_assert(kDma0 + kPieces <= N, "DMA pieces past the tile");
-  static_assert(kNx + kLA - 1 <= N - 1 - kLA, "next tile's operands must be covered by the last MFMA's wait");
+  // R = 2
+  static constexpr int kG1 = R == 2 ? kC - L : -1, kG2 = R == 2 ? N - L : -1;
+  static constexpr int kHalf = kPieces / 2;                    // pieces per half-tile batch
+  static constexpr int kP0 = 0, kP1 = kG1 + 1;                 // first gaps of the two batches
+  static constexpr int kList = R == 4 ? kGb - 6 : kG2 - 4;     // the key block of tile t+3 (R=4) / t+2
+  static constexpr int kNx = R == 4 ? kGb + 1 : kG2;           // tile t+1's first operands
+  static_assert(R == 2 || kGb >= kC, "the barrier must follow the reads of the previous tile");
+  static_assert(R == 2 || kDma0 + kPieces <= N, "DMA pieces past the tile");
+  static_assert(R == 4 || (kP1 + kHalf <= kG2 && kHalf <= kG1), "DMA batches overlap a barrier");
+  static_assert(kNx + L - 1 <= N - 1 || R == 2, "next tile's operands must be covered by the last MFMA's wait");
+  static_assert(R == 4 || kNx + L == N, "next tile's operands are read after G2");
   static constexpr int sec(int g) { return g < kB ? 0 : g < kC ? 1 : g < kD ? 2 : 3; }
   static constexpr int sec0(int c) { return c == 0 ? 0 : c == 1 ? kB : c == 2 ? kC : kD; }
   static constexpr int op_reads(int g) { return (sec(g) & 1) ? 2 : 1; }
-  static constexpr int extra_reads(int h) { return (h == kList || (h >= kNx && h < kNx + kLA)) ? 1 : 0; }
-  static constexpr int gap_reads(int h) { return (h + kLA < N ? op_reads(h + kLA) : 0) + extra_reads(h); }
+  static constexpr int extra_reads(int h) { return (h == kList || (h >= kNx && h < kNx + L)) ? 1 : 0; }
+  static constexpr int gap_reads(int h) { return (h + L < N ? op_reads(h + L) : 0) + extra_reads(h); }
+  // lgkmcnt before MFMA g (reads issued after g's operand; a barrier's drain only lowers the count).
+  // MFMAs g < L take the operands read at the end of the previous tile (nx): R = 4 reads them early
+  // enough that the last MFMAs' waits cover them; R = 2 reads them after G2 and waits here.
   static constexpr int wait_n(int g) {
-    if (g < kLA) return 15;
-    int n = extra_reads(g - kLA);
-    for (int h = g - kLA + 1; h < g; ++h) n += gap_reads(h);
+    if (g < L && R == 4) return 15;
+    if (g < L) {
+      int n = N - 1 - (kNx + g);
+      for (int h = 0; h < g; ++h) n += gap_reads(h);
+      return n > 15 ? 15 : n;
+    }
+    int n = extra_reads(g - L);
+    for (int h = g - L + 1; h < g; ++h) n += gap_reads(h);
     return n > 15 ? 15 : n;
   }
-  static_assert(extra_reads(kGb) == 0, "no read beside the barrier");
+  static_assert(R == 2 || extra_reads(kGb) == 0, "no read beside the barrier");
+  static_assert(R == 4 || kList < kG2, "the list entry is read before G2's drain");
 };
 
 // d = a . b(AGPR) + c (c a separate VGPR tile: the dP^T chain's -Delta seeds, which hipcc
@@ -315,23 +351,25 @@ __device__ __forceinline__ void mf_cacc(f32x16& d, const typename T::vec8& a, co
 }
 // op k (0..55) of one 32-key half of the dQ pass: P = exp2(S c + nL), dS = P * dP (dP seeded with
 // -Delta), pd = bf16 pairs of dS (the B operand of dQ^T += K^T.dS^T)
-template <class T, int k>
-__device__ __forceinline__ void qop(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl) {
+// kSeeded = false (the R = 2 kernel, whose registers do not hold a -Delta seed tile): dP starts
+// from zero and dS = P * (dP + nd), nd = -Delta of the lane's row
+template <class T, bool kSeeded, int k>
+__device__ __forceinline__ void qop(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl, float nd) {
   constexpr int st = k >> 4, r = k & 15;
   if constexpr (st == 0) s[r] = fmaf(s[r], c, nl);
   else if constexpr (st == 1) s[r] = exp2_fast(s[r]);
-  else if constexpr (st == 2) dp[r] = dp[r] * s[r];
+  else if constexpr (st == 2) dp[r] = kSeeded ? dp[r] * s[r] : (dp[r] + nd) * s[r];
   else pd[r >> 2][r & 3] = pack2<T>(dp[2 * r], dp[2 * r + 1]);
 }
-template <class T, int lo, int... Ks>
-__device__ __forceinline__ void qops_at(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl,
+template <class T, bool kSeeded, int lo, int... Ks>
+__device__ __forceinline__ void qops_at(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl, float nd,
                                         std::integer_sequence<int, Ks...>) {
-  (qop<T, lo + Ks>(s, dp, pd, c, nl), ...);
+  (qop<T, kSeeded, lo + Ks>(s, dp, pd, c, nl, nd), ...);
 }
-template <class T, int i, int n>
-__device__ __forceinline__ void qgap(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl) {
+template <class T, bool kSeeded, int i, int n>
+__device__ __forceinline__ void qgap(f32x16& s, f32x16& dp, u32x4 (&pd)[2], float c, float nl, float nd) {
   constexpr int lo = i * 56 / n, hi = (i + 1) * 56 / n;
-  qops_at<T, lo>(s, dp, pd, c, nl, std::make_integer_sequence<int, hi - lo>{});
+  qops_at<T, kSeeded, lo>(s, dp, pd, c, nl, nd, std::make_integer_sequence<int, hi - lo>{});
 }
 
 }  // namespace kvp
@@ -819,14 +857,19 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
 // dK/dV kernel above (QSched). Keys past a tile's end read as zero rows (buffer extent), which add
 // nothing to dQ (dQ^T += K^T.dS^T with K = 0).
 // ------------------------------------------------------------------------------------------------
-template <int D, class T, bool kPool>
-__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) bwd_dq_pipe_kernel(const BwdParams p) {
+// R = 4: the 4-slot ring (one workgroup per CU at D=128); R = 2: the 2-slot ring with half-tile DMA
+// batches, two workgroups per CU (QSched)
+template <int D, class T, bool kPool, int R>
+__global__ void __launch_bounds__(bwd::kThreads, R == 2 ? 2 : (D == 128 ? 1 : VB_KV64_WAVES))
+    bwd_dq_pipe_kernel(const BwdParams p) {
   using namespace bwd;
   using namespace kvp;
-  using S = QSched<D>;
+  using S = QSched<D, R, R == 2 ? VB_DQ2_LA : kLA>;
   using V8 = typename T::vec8;
   constexpr int KS = S::KS, DT = S::DT, RB = S::RB, N = S::N, TB = S::kTileBytes;
   constexpr int kPieces = S::kPieces, kPQ = S::kPQ;
+  constexpr int kLA = S::LA;              // shadows kvp::kLA
+  constexpr bool kSeeded = R == 4;        // R = 2 holds no -Delta seed tile (qop)
   __shared__ __attribute__((aligned(16))) uint8_t smem[S::kLdsBytes];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + S::kListOff);
   int* list_n = reinterpret_cast<int*>(smem + S::kListOff + 2 * kMaxBlocks);   // [4] + chunk counts
@@ -948,12 +991,15 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     const int kpbytes = kPool ? (int)((int64_t)(p.Lkp - 1) * kprowb + RB) : 0;
     const int vpbytes = kPool ? (int)((int64_t)(p.Lkp - 1) * vprowb + RB) : 0;
     // piece k of this wave: K rows kRpp (wave + 4k).. (k < kPQ), V rows kRpp (wave + 4(k-kPQ))..;
-    // the lane's voffset per key source (main / pooled row strides)
-    int voff_m[kPieces], voff_p[kPieces];
+    // the lane's voffset per key source (main / pooled row strides). R = 2 keeps piece 0's only:
+    // the swizzle depends on row bits the piece index does not touch (rows differ by 4 kRpp k), so
+    // piece k adds 4 kRpp k rows as a scalar offset (TileDma::krb / vrb)
+    constexpr int kVo = R == 2 ? 2 : kPieces;
+    int voff_m[kVo], voff_p[kVo];
 #pragma unroll
-    for (int k = 0; k < kPieces; ++k) {
-      const bool isv = k >= kPQ;
-      const int r = (wave + 4 * (k % kPQ)) * S::kRpp + lane / (RB / 16);
+    for (int k = 0; k < kVo; ++k) {
+      const bool isv = R == 2 ? k == 1 : k >= kPQ;
+      const int r = (wave + 4 * (R == 2 ? 0 : k % kPQ)) * S::kRpp + lane / (RB / 16);
       const int c16 = 16 * ((lane % (RB / 16)) ^ dual_swz<D>(r));
       voff_m[k] = r * (isv ? vrowb : krowb) + c16;
       voff_p[k] = r * (isv ? vprowb : kprowb) + c16;
@@ -961,6 +1007,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     struct TileDma {
       srd_t k, v;
       int soff_k, soff_v;
+      int krb, vrb;   // row strides (R = 2)
       bool pooled;
     };
     // tile tt's source: kept block list[tt/2] half tt%2, then pooled tiles; past the end zero-extent
@@ -996,21 +1043,31 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
       const uint32_t vlo = sm.vlo ^ (sx.vlo & (uint32_t)pm), vhi = sm.vhi ^ (sx.vhi & (uint32_t)pm);
       d.k = srd_t{reinterpret_cast<const void*>(((uint64_t)khi << 32) | klo), (sm.kbytes ^ (sx.kbytes & pm)) & lm};
       d.v = srd_t{reinterpret_cast<const void*>(((uint64_t)vhi << 32) | vlo), (sm.vbytes ^ (sx.vbytes & pm)) & lm};
-      d.soff_k = kstart * (sm.krowb ^ (sx.krowb & pm));
-      d.soff_v = kstart * (sm.vrowb ^ (sx.vrowb & pm));
+      d.krb = sm.krowb ^ (sx.krowb & pm);
+      d.vrb = sm.vrowb ^ (sx.vrowb & pm);
+      d.soff_k = kstart * d.krb;
+      d.soff_v = kstart * d.vrb;
       return d;
     };
     auto piece = [&](const TileDma& d, int slot, int k) __attribute__((always_inline)) {
-      int vo = voff_m[k];
+      const int kv = R == 2 ? (k >= kPQ) : k;
+      int vo = voff_m[kv];
       if constexpr (kPool) {   // one v_bfi on a uniform mask; a select here becomes a branch per piece
         int pm = uniform(d.pooled ? -1 : 0);
 #if __HIP_DEVICE_COMPILE__
         asm volatile("" : "+s"(pm));
 #endif
-        vo = (pm & voff_p[k]) | (~pm & vo);
+        vo = (pm & voff_p[kv]) | (~pm & vo);
       }
-      if (k < kPQ) dma16(d.k, smem + S::kKOff + slot * TB + (wave + 4 * k) * 1024, vo, d.soff_k);
-      else dma16(d.v, smem + S::kVOff + slot * TB + (wave + 4 * (k - kPQ)) * 1024, vo, d.soff_v);
+      const int kk = k < kPQ ? k : k - kPQ;
+      const int radd = R == 2 ? 4 * S::kRpp * kk : 0;   // rows past piece 0 (scalar)
+      if (k < kPQ) dma16(d.k, smem + S::kKOff + slot * TB + (wave + 4 * k) * 1024, vo, d.soff_k + radd * d.krb);
+      else dma16(d.v, smem + S::kVOff + slot * TB + (wave + 4 * kk) * 1024, vo, d.soff_v + radd * d.vrb);
+    };
+    // piece j (0..kHalf-1) of half h's batch: K pieces h kPQ/2.., then V pieces kPQ + h kPQ/2..
+    auto half_piece = [&](const TileDma& d, int slot, int h, int j) __attribute__((always_inline)) {
+      constexpr int kq = kPQ / 2;
+      piece(d, slot, j < kq ? h * kq + j : kPQ + h * kq + (j - kq));
     };
     auto list_at = [&](int tt) __attribute__((always_inline)) -> int {
       return __builtin_amdgcn_readfirstlane((int)list[max(min(tt >> 1, nkept - 1), 0)]);
@@ -1018,7 +1075,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
 
     const uint32_t sbase = static_cast<uint32_t>(
         reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint8_t*)smem));
-    constexpr bool kShare = S::kVOff + 3 * TB + 48 * RB < 65536;
+    constexpr bool kShare = S::kVOff + (R - 1) * TB + 48 * RB < 65536;
     constexpr int NA = kShare ? 1 : 2;
     constexpr int kVImm = kShare ? S::kVOff : 0;
     uint32_t xa[NA][KS];       // [K, V][ks]: key row l32, chunk 2 ks + half
@@ -1041,31 +1098,48 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     const float c = p.c;
 
     f32x16 s0, dp0, s1, dp1;   // S^T / dP^T of keys 0-31 and 32-63 (lane = query)
-    f32x16 cdt;                // -Delta seeds of the current tile's key source
+    f32x16 cdt;                // -Delta seeds of the current tile's key source (kSeeded)
     float nl0 = 0.f, nl1 = 0.f;   // -L' of the tile whose V(t,0) / V(t,1) runs
+    float nd0 = 0.f, nd1 = 0.f;   // -Delta of the same (!kSeeded)
     u32x4 pd0[2], pd1[2];
     V8 nx[kLA];
     uint32_t blk_raw = 0;
     TileDma dn{};
     auto set_class = [&](bool pooled) __attribute__((always_inline)) {
       const float dr = pooled ? opaque(D2) : opaque(D1);
+      if constexpr (kSeeded) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) cdt[r] = dr;
-      launder(cdt);   // kept in 16 registers: hipcc would rebuild the broadcast with 16 v_movs per tile
+        for (int r = 0; r < 16; ++r) cdt[r] = dr;
+        launder(cdt);   // kept in 16 registers: hipcc would rebuild the broadcast with 16 v_movs per tile
+      } else {
+        nd0 = dr;
+      }
       nl0 = pooled ? -opaque(L2) : -opaque(L1);
     };
 
-    // ---- prologue: tiles 0-2 in flight, tile 0 landed, its first operands read ---------------
-    dn = tile_dma(0, list_at(0));
+    if constexpr (R == 4) {
+      // ---- prologue: tiles 0-2 in flight, tile 0 landed, its first operands read -------------
+      dn = tile_dma(0, list_at(0));
 #pragma unroll
-    for (int k = 0; k < kPieces; ++k) piece(dn, 0, k);
-    dn = tile_dma(1, list_at(1));
+      for (int k = 0; k < kPieces; ++k) piece(dn, 0, k);
+      dn = tile_dma(1, list_at(1));
 #pragma unroll
-    for (int k = 0; k < kPieces; ++k) piece(dn, 1, k);
-    dn = tile_dma(2, list_at(2));
+      for (int k = 0; k < kPieces; ++k) piece(dn, 1, k);
+      dn = tile_dma(2, list_at(2));
 #pragma unroll
-    for (int k = 0; k < kPieces; ++k) piece(dn, 2, k);
-    VB_WAIT_VMCNT(2 * kPieces);
+      for (int k = 0; k < kPieces; ++k) piece(dn, 2, k);
+      VB_WAIT_VMCNT(2 * kPieces);
+    } else {
+      // ---- prologue: both halves of tile 0 in flight, half 0 landed; dn = tile 1 (its halves
+      // are issued in tile 0, at gaps kP0.. and after G1) ---------------------------------------
+      dn = tile_dma(0, list_at(0));
+#pragma unroll
+      for (int j = 0; j < S::kHalf; ++j) half_piece(dn, 0, 0, j);
+#pragma unroll
+      for (int j = 0; j < S::kHalf; ++j) half_piece(dn, 0, 1, j);
+      dn = tile_dma(1, list_at(1));
+      VB_WAIT_VMCNT(S::kHalf);
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd128<0>(nx[0], xa[0][0]);
@@ -1080,24 +1154,34 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     set_class(kPool && 0 >= ntm);
 
     auto iter = [&](int t, auto U, auto M) __attribute__((always_inline)) {
-      constexpr int u = decltype(U)::value;
-      constexpr int up = (u + 3) & 3, un = (u + 1) & 3;
+      constexpr int u = decltype(U)::value % R;   // tile t's ring slot (t mod R)
+      constexpr int up = (u + R - 1) % R, un = (u + 1) % R;
       constexpr int mode = decltype(M)::value;
       V8 xop[N];
       s16x4 ylo[N], yhi[N];
       auto gap = [&](auto G) __attribute__((always_inline)) {
         constexpr int g = decltype(G)::value;
         constexpr int sc = S::sec(g), i = g - S::sec0(S::sec(g));
+        // R = 2: the half-tile barriers come before the gap's reads (QSched)
+        auto half_barrier = [&]() __attribute__((always_inline)) {
+#if __HIP_DEVICE_COMPILE__
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+          VB_WAIT_VMCNT(S::kHalf);
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        };
         // ---- MFMA g ----
         if constexpr (sc == 0 || sc == 2) {
           V8& a = g < kLA ? nx[g % kLA] : xop[g];
-          if constexpr (g >= kLA) wait1<S::wait_n(g)>(a);
+          if constexpr (g >= kLA || R == 2) wait1<S::wait_n(g)>(a);
           if constexpr (mode != 2) {
             f32x16& s_ = sc == 0 ? s0 : s1;
             f32x16& dp = sc == 0 ? dp0 : dp1;
             constexpr int ks = i >> 1;
             if constexpr (i & 1) {
-              if constexpr (ks == 0) mf_cacc<T>(dp, a, df[0], cdt);
+              if constexpr (ks == 0 && kSeeded) mf_cacc<T>(dp, a, df[0], cdt);
+              else if constexpr (ks == 0) mf_zero<T>(dp, a, df[0]);
               else mf_vacc<T>(dp, a, df[ks]);
             } else {
               if constexpr (ks == 0) mf_zero<T>(s_, a, qf[0]);
@@ -1114,6 +1198,12 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (R == 2 && mode != 2 && g == S::kG1) half_barrier();
+        if constexpr (R == 2 && mode != 2 && g == S::kG2) {
+          half_barrier();
+          launder(blk_raw);
+          dn = tile_dma(t + 2, __builtin_amdgcn_readfirstlane((int)blk_raw));   // for tile t+1's batches
+        }
         // ---- fillers of gap g ----
         constexpr int m = g + kLA;
         if constexpr (m < N) {
@@ -1130,27 +1220,35 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
             rdtr<imm>(yhi[m], ya[dt][1]);
           }
         }
-        if constexpr (g == S::kList) rdu16(blk_raw, lista + 2 * max(min((t + 3) >> 1, nkept - 1), 0));
+        if constexpr (g == S::kList) rdu16(blk_raw, lista + 2 * max(min((t + (R == 4 ? 3 : 2)) >> 1, nkept - 1), 0));
         if constexpr (g >= S::kNx && g < S::kNx + kLA) {
           constexpr int q = g - S::kNx;
           rd128<un * TB + ((q & 1) ? kVImm : 0)>(nx[q], xa[(q & 1) && !kShare][q >> 1]);
         }
         // ---- score arithmetic ----
-        if constexpr (mode != 2 && g >= S::kV0 && g < S::kV0 + S::kV0n) qgap<T, g - S::kV0, S::kV0n>(s0, dp0, pd0, c, nl0);
+        if constexpr (mode != 2 && g >= S::kV0 && g < S::kV0 + S::kV0n)
+          qgap<T, kSeeded, g - S::kV0, S::kV0n>(s0, dp0, pd0, c, nl0, nd0);
         if constexpr (mode != 2 && g >= S::kV1) {
-          if constexpr (g == S::kV1) nl1 = nl0;
-          qgap<T, g - S::kV1, S::kV1n>(s1, dp1, pd1, c, nl1);
+          if constexpr (g == S::kV1) {
+            nl1 = nl0;
+            nd1 = nd0;
+          }
+          qgap<T, kSeeded, g - S::kV1, S::kV1n>(s1, dp1, pd1, c, nl1, nd1);
         }
-        if constexpr (mode != 1 && g < S::kV1 + S::kV1n - N) qgap<T, g + N - S::kV1, S::kV1n>(s1, dp1, pd1, c, nl1);
-        // ---- barrier and the DMA of tile t+3 into the slot tile t-1 left ----
-        if constexpr (mode != 2 && g == S::kGb) {
+        if constexpr (mode != 1 && g < S::kV1 + S::kV1n - N)
+          qgap<T, kSeeded, g + N - S::kV1, S::kV1n>(s1, dp1, pd1, c, nl1, nd1);
+        // ---- R = 2: the two half-tile batches of tile t+1 into the slot tile t-1 left ----
+        if constexpr (R == 2 && mode != 2 && g >= S::kP0 && g < S::kP0 + S::kHalf) half_piece(dn, up, 0, g - S::kP0);
+        if constexpr (R == 2 && mode != 2 && g >= S::kP1 && g < S::kP1 + S::kHalf) half_piece(dn, up, 1, g - S::kP1);
+        // ---- R = 4: barrier and the DMA of tile t+3 into the slot tile t-1 left ----
+        if constexpr (R == 4 && mode != 2 && g == S::kGb) {
           VB_WAIT_VMCNT(kPieces);   // tile t+1 landed (tile t+2 may be in flight)
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
           launder(blk_raw);
           dn = tile_dma(t + 3, __builtin_amdgcn_readfirstlane((int)blk_raw));
         }
-        if constexpr (mode != 2 && g >= S::kDma0 && g < S::kDma0 + kPieces) piece(dn, up, g - S::kDma0);
+        if constexpr (R == 4 && mode != 2 && g >= S::kDma0 && g < S::kDma0 + kPieces) piece(dn, up, g - S::kDma0);
         if constexpr (g == N - 1) {
 #pragma unroll
           for (int q = 0; q < kLA; ++q) launder(nx[q]);
@@ -1239,21 +1337,31 @@ bool dq_pipe_enabled(int D) {
   return D == 128 ? on128 : on64;
 }
 
-template <int D>
+template <int D, int R>
 static int launch_dq(const BwdParams& p, bool pool, bool f16, hipStream_t s) {
   const dim3 grid(p.nbq * p.B * p.H);
   if (pool) {
-    if (f16) hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, F16, true>), grid, dim3(bwd::kThreads), 0, s, p);
-    else hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, BF16, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    if (f16) hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, F16, true, R>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, BF16, true, R>), grid, dim3(bwd::kThreads), 0, s, p);
   } else {
-    if (f16) hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, F16, false>), grid, dim3(bwd::kThreads), 0, s, p);
-    else hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, BF16, false>), grid, dim3(bwd::kThreads), 0, s, p);
+    if (f16) hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, F16, false, R>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, BF16, false, R>), grid, dim3(bwd::kThreads), 0, s, p);
   }
   return check_launch("bwd_dq_pipe_kernel");
 }
 
+// D=128: the ring of VB_BWD_DQ128_RING slots (VB_BWD_DQ128_RING=2|4 in the environment)
+static int dq128_ring() {
+  static const int r = [] {
+    const char* e = getenv("VB_BWD_DQ128_RING");
+    return (e ? atoi(e) : VB_BWD_DQ128_RING) == 2 ? 2 : 4;
+  }();
+  return r;
+}
+
 int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s) {
-  return D == 128 ? launch_dq<128>(p, pool, f16, s) : launch_dq<64>(p, pool, f16, s);
+  if (D == 64) return launch_dq<64, 4>(p, pool, f16, s);
+  return dq128_ring() == 2 ? launch_dq<128, 2>(p, pool, f16, s) : launch_dq<128, 4>(p, pool, f16, s);
 }
 
 int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream_t s) {

@@ -119,7 +119,8 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     bh = blockIdx.x % BH;
   } else {
     const int rows_left = p.nbq - hr;
-    const int lin = xcd_linear(blockIdx.x - n_heavy, rows_left * BH);
+    int lin = xcd_linear(blockIdx.x - n_heavy, rows_left * BH);
+    if (p.q_order) lin = __builtin_amdgcn_readfirstlane(p.q_order[lin]);   // longest first (attn_order_kernel)
     bh = lin / rows_left;
     qblk = rows_left - 1 - lin % rows_left;
   }
@@ -969,6 +970,89 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   VB_ATRACE_END();
 }
 
+// Dispatch order of the attention kernel's phase 2 (longest-processing-time first, per XCD): the
+// kernel deals workgroups round-robin over the 8 XCDs and gives XCD x the contiguous range of
+// linear work items xcd_linear assigns it (head-major). Each XCD drains its range in order, so its
+// last workgroups set the kernel's tail. One workgroup per XCD range re-sorts the range by (head,
+// kept key blocks descending): the head-major grouping (the L2 reuse of a head's K/V) stays, and
+// within every head the longest q-blocks go first and the shortest last. Counting sort over
+// (head, length) bins in LDS; the order inside a bin follows the atomics (placement only: every
+// q-block's output is the same whatever the order). order[start + rank] = item.
+constexpr int kOrderBins = 8192;
+__global__ void __launch_bounds__(1024) attn_order_kernel(const FwdParams p, int32_t* order) {
+  __shared__ int bins[kOrderBins];
+  const int BH = p.B * p.H;
+  const int hr = min(p.heavy_rows, p.nbq);
+  const int rows_left = p.nbq - hr;
+  const int nwg = rows_left * BH;
+  const int x = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  int start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+  const int count_x = q8 + (x < r8 ? 1 : 0);
+  if (count_x <= 0) return;
+  // only the range's last `order_window` items are re-ordered (the rest keep their place)
+  const int skip = (p.order_window > 0 && p.order_window < count_x) ? count_x - p.order_window : 0;
+  for (int i = threadIdx.x; i < skip; i += blockDim.x) order[start + i] = start + i;
+  start += skip;
+  const int count = count_x - skip;
+  const int bh0 = start / rows_left;
+  const int nh = (start + count - 1) / rows_left - bh0 + 1;
+  const int nl = p.nbk + 1;   // kept counts 0..nbk
+  if ((int64_t)nh * nl > kOrderBins) {   // too many bins for LDS: keep the kernel's own order
+    for (int i = threadIdx.x; i < count; i += blockDim.x) order[start + i] = start + i;
+    return;
+  }
+  for (int i = threadIdx.x; i < nh * nl; i += blockDim.x) bins[i] = 0;
+  __syncthreads();
+  auto key_of = [&](int lin) -> int {
+    const int bh = lin / rows_left, qblk = rows_left - 1 - lin % rows_left;
+    bool nan_head = false;
+    const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, bh / p.H, bh % p.H, nan_head, p.hm_mode);
+    int kept = p.nbk;
+    if (p.q_len) {
+      kept = min(max(p.q_len[(int64_t)bh * p.nbq + qblk], 0), p.nbk);
+    } else if (mh) {
+      const uint8_t* mrow = mh + (int64_t)qblk * p.ms[2];
+      kept = 0;
+      for (int j = 0; j < p.nbk; ++j) kept += mrow[j] != 0;
+    }
+    return (bh - bh0) * nl + (p.nbk - kept);   // head ascending, kept count descending
+  };
+  for (int i = threadIdx.x; i < count; i += blockDim.x) atomicAdd(&bins[key_of(start + i)], 1);
+  __syncthreads();
+  {   // exclusive prefix over the bins: every thread a run of C bins, a scan of the runs' sums
+    __shared__ int wsum[16];
+    const int nbins = nh * nl;
+    const int C = (nbins + 1023) / 1024;
+    const int b0 = threadIdx.x * C;
+    int run = 0;
+    for (int i = 0; i < C; ++i) run += (b0 + i < nbins) ? bins[b0 + i] : 0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = run;   // inclusive scan within the wave
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int i = 0; i < w; ++i) wbase += wsum[i];
+    int pos = wbase + incl - run;   // exclusive prefix of this thread's run
+    for (int i = 0; i < C; ++i) {
+      if (b0 + i < nbins) {
+        const int c = bins[b0 + i];
+        bins[b0 + i] = pos;
+        pos += c;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < count; i += blockDim.x) {
+    const int lin = start + i;
+    order[start + atomicAdd(&bins[key_of(lin)], 1)] = lin;
+  }
+}
+
 template <int D, class T>
 static int launch_fwd(const FwdParams& p, bool pool, hipStream_t stream) {
   const dim3 grid(p.nbq * p.B * p.H);
@@ -1076,6 +1160,14 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
 #if VB_DIAG
   if (const char* d = getenv("VB_DEBUG_ATTN")) p.dbg = atoi(d);
 #endif
+  p.q_len = a->q_lengths;
+  p.order_window = a->order_window;
+  if (a->q_order && p.use_main && p.mask) {   // longest-first dispatch order (scheduling only)
+    hipLaunchKernelGGL(attn_order_kernel, dim3(8), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), p,
+                       a->q_order);
+    if (int rc = check_launch("attn_order_kernel")) return rc;
+    p.q_order = a->q_order;
+  }
   return dispatch_fwd(p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream));
 }
 

@@ -20,6 +20,9 @@ struct FwdParams {
   int B, H, Lq, Lk, nbq, nbk;
   float c;                                    // softmax scale * log2(e)
   int heavy_rows;                             // last q-block rows known to be dense (scheduling hint)
+  const int32_t* q_order;                     // phase-2 dispatch order (attn_order_kernel), or NULL
+  const int32_t* q_len;                       // kept key blocks per mask row (ordering input), or NULL
+  int order_window;                           // re-order only the last N items of each XCD range (0: all)
   // multi-level mode (vb_ml_attn_fwd): k/v are the KV pyramids [B,H,15*Lpad/8,D]
   int Lpad;                                   // level-1 rows (ceil(L/128)*128)
   int ref_tail;                               // 1: level-1 tail keys >= L take part (zero rows)

@@ -112,6 +112,7 @@ struct PredParams {
   void* po;
   uint8_t* mask;
   unsigned long long* count;
+  int32_t* rows_kept;   // [B,H,nb] kept blocks per mask row (nullable)
   int dbg;   // diagnostic builds only (VB_DEBUG_PRED): 1 = skip epilogue, 2 = skip main loop, 4 = no MFMA
 };
 
@@ -845,6 +846,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     const bool force_all = p.force_tail > 0 && qb >= nb - p.force_tail;
     const int kept = energy_row<T>(val, keys, mrow, nb, p.thr, p.min_keep, p.max_keep, p.force_tail, force_all);
     if (p.count && lane == 0) atomicAdd(p.count, (unsigned long long)kept);
+    if (p.rows_kept && lane == 0) p.rows_kept[(int64_t)bh * nb + qb] = kept;
   };
 #pragma unroll
   for (int e = 0; e < KQ; ++e)
@@ -993,6 +995,7 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   p.thr = a->energy_threshold;
   p.min_keep = a->min_keep; p.max_keep = a->max_keep; p.force_tail = a->force_tail;
   p.po = a->po; p.mask = a->mask; p.count = a->mask_count;
+  p.rows_kept = a->mask_level ? nullptr : a->mask_rows_kept;
   p.q_s = nullptr;
   p.k_s = reinterpret_cast<uint8_t*>(a->workspace);
   p.rbuf = reinterpret_cast<uint16_t*>(p.k_s + rows_b);

@@ -37,6 +37,7 @@ class AttnArgs(ctypes.Structure):
         ("scale", ctypes.c_float),
         ("dtype", ctypes.c_int),
         ("heavy_rows", ctypes.c_int),
+        ("q_order", _vp), ("q_lengths", _vp), ("order_window", ctypes.c_int),
     ]
 
 
@@ -61,6 +62,7 @@ class PredictArgs(ctypes.Structure):
         ("philox", ctypes.c_int), ("philox_seed", ctypes.c_uint64), ("philox_offset", ctypes.c_uint64),
         ("mask_level", ctypes.c_int), ("level_bands", ctypes.c_int),
         ("level_band_value", _vp), ("level_band_start", _vp), ("level_band_end", _vp),
+        ("mask_rows_kept", _vp),
     ]
 
 
@@ -196,7 +198,7 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.vb_abi_version() != 2:
+    if lib.vb_abi_version() != 3:
         raise VBladeError("libvblade_hip.so ABI version mismatch")
     _lib = lib
     return lib

@@ -39,6 +39,14 @@ VARIANT_DEFAULTS = {
 }
 
 
+# longest-first dispatch of the attention launch (one small ordering launch before it), per
+# variant. Measured (tools/ab.py, round 5, profiles/r05_attn_order_ab.log): Wan 1.047-1.054x per
+# attention launch; CogVideoX 0.98x over the whole range and 0.976-0.989x with only the last
+# 64-256 q-blocks of each XCD range re-ordered (its q-blocks differ little in length, and the
+# Gilbert-neighbour order's L2 reuse and the extra launch cost more than the tail)
+ORDER_DEFAULT = {"cog": False, "wan": True}
+
+
 def retain_counts(nb: int, min_ratio: float, max_ratio: float, variant: str):
     """Kept-block clamp bounds. cog: (seq * fp32 ratio tensor).to(int) clamped >= 1
     (cogvideo_blocksparseattn.py:230-231, 347-348); wan: max(1, int(seq * ratio)) (wanx :215-216)."""
@@ -122,7 +130,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
             raise ValueError(f"variant must be one of {list(VARIANT_DEFAULTS)}")
         cfg = dict(VARIANT_DEFAULTS[variant])
         unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep", "overlap", "gather_kv",
-                                               "mask_head_mode"}
+                                               "mask_head_mode", "order", "order_window"}
         if unknown:
             raise TypeError(f"unknown options {sorted(unknown)}")
         cfg.update(overrides)
@@ -165,6 +173,13 @@ class AdaptiveBlockSparseAttn(nn.Module):
         # (tools/diag/overlap_ab.py --opt gather_kv): gather at D=128 (Wan, +2.4 % per call), copies at
         # D=64 (CogVideoX, +0.9 %).
         self.gather_kv = cfg.get("gather_kv", "auto")
+        # Dispatch each XCD's q-blocks of the attention launch longest first (the predictor writes
+        # every mask row's kept-block count; a small launch sorts the XCD ranges before the kernel):
+        # the kernel's tail is its last workgroups. Scheduling only: outputs are bit-identical.
+        # order_window > 0 re-orders only each XCD range's last q-blocks (the tail), keeping the
+        # head-major Gilbert-neighbour order elsewhere for its L2 reuse.
+        self.order = bool(cfg.get("order", ORDER_DEFAULT[variant]))
+        self.order_window = int(cfg.get("order_window", 0))
 
     # -------------------------------------------------------------------------------- helpers
     def _rows(self, device):
@@ -215,7 +230,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
         return float(torch.log(torch.tensor(float(self.sample_gap), dtype=dtype)).item())
 
     # -------------------------------------------------------------------------------- forward
-    def predict_mask(self, q, k, q_off=None, k_off=None, count=None, staged_event=None, pool=None):
+    def predict_mask(self, q, k, q_off=None, k_off=None, count=None, staged_event=None, pool=None,
+                     rows_kept=None):
         """Block mask [B,H,nb,nb] (uint8, Gilbert order) and normalised pooled scores. ``pool``
         (v, gap, outs) runs the pooled K/V pass inside the score kernel's launch."""
         B, H, L, D = q.shape
@@ -237,7 +253,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
                                     energy_threshold=self.energy_threshold, min_keep=lo,
                                     max_keep=hi, force_tail=self.force_tail, mask_count=count,
                                     staged_event=staged_event, rand=rand, philox=philox,
-                                    pool=pool)
+                                    pool=pool, rows_kept=rows_kept)
         return po, mask
 
     def forward(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *,
@@ -258,6 +274,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
         grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)
         fused = not grad and self.combine != "reference"
         pooled = None
+        rows_kept = None
         if block_mask is None:
             # inference: the pooled K/V pass (one pass over K/V: pooled K/V + the Gilbert-ordered
             # contiguous copies the attention kernel streams by LDS-DMA; HBM-bound) runs inside the
@@ -267,9 +284,12 @@ class AdaptiveBlockSparseAttn(nn.Module):
             gather = self._gather(D)
             copies = not (gather and rows is not None)
             outs = ops.pool_kv_outputs(k, self.sample_gap, reordered=copies) if ride else None
+            if fused and self.order and self.mask_head_mode == "per_head":
+                rows_kept = torch.empty(B, H, nb, device=q.device, dtype=torch.int32)
             with torch.no_grad():
                 _, mask = self.predict_mask(q.detach(), k.detach(), q_off, k_off, count,
-                                            pool=(v, self.sample_gap, outs) if ride else None)
+                                            pool=(v, self.sample_gap, outs) if ride else None,
+                                            rows_kept=rows_kept)
             if ride:
                 pooled = outs
             elif fused:
@@ -309,7 +329,8 @@ class AdaptiveBlockSparseAttn(nn.Module):
                 e0.record()
             out = ops.attention_fwd(q, k_src, v_src, block_mask=mask, q_rows=rows, kv_rows=kv_rows,
                                     kp=kp, vp=vp, kp_log_bias=self._log_gap(q.dtype),
-                                    heavy_rows=self.force_tail)
+                                    heavy_rows=self.force_tail, order=self.order, q_lengths=rows_kept,
+                                    order_window=self.order_window)
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()

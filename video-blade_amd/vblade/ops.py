@@ -89,9 +89,13 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
                   kv_rows: Optional[torch.Tensor] = None, kp: Optional[torch.Tensor] = None,
                   vp: Optional[torch.Tensor] = None, kp_log_bias: float = 0.0, use_main: bool = True,
                   scale: Optional[float] = None, need_lse: bool = False,
-                  out: Optional[torch.Tensor] = None, heavy_rows: int = 0):
+                  out: Optional[torch.Tensor] = None, heavy_rows: int = 0, order: bool = False,
+                  q_lengths: Optional[torch.Tensor] = None, order_window: int = 0):
     """vb_attn_fwd: softmax over (block-masked keys of k/v) ∪ (pooled keys kp/vp + bias).
     q,k,v [B,H,L,D]; block_mask [B,H,ceil(Lq/128),ceil(Lk/128)] bool/uint8; rows int32.
+    ``order``: dispatch each XCD's q-blocks longest first (scheduling only; ``q_lengths`` [B,H,nbq]
+    int32 kept blocks per mask row from mask_predict(rows_kept=...), else counted on the device;
+    ``order_window`` > 0 re-orders only the last that many q-blocks of each XCD's range).
     Returns out [B,H,Lq,D] (and lse fp32 [B,H,Lq] when need_lse)."""
     dev = _require_gpu(q, k, v, block_mask, q_rows, kv_rows, kp, vp)
     q = _aligned_bhld(q)
@@ -137,6 +141,15 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
     a.scale = float(scale) if scale else 0.0
     a.dtype = _dtype_code(q)
     a.heavy_rows = int(heavy_rows)
+    if order and block_mask is not None and use_main:
+        nbq = (Lq + BLOCK - 1) // BLOCK
+        q_order = torch.empty(B * H * nbq, device=dev, dtype=torch.int32)   # workspace
+        a.q_order = q_order.data_ptr()
+        a.order_window = int(order_window)
+        if q_lengths is not None:
+            if q_lengths.dtype != torch.int32 or q_lengths.numel() != B * H * nbq or not q_lengths.is_contiguous():
+                raise ValueError("attention_fwd: q_lengths must be contiguous int32 [B,H,ceil(Lq/128)]")
+            a.q_lengths = q_lengths.data_ptr()
     check(_lib.load().vb_attn_fwd(ctypes.byref(a), _stream(dev)), "vb_attn_fwd")
     return (out, lse) if need_lse else out
 
@@ -298,7 +311,8 @@ def block_sparse_attn_bwd(dout, q_unpad, k_unpad, v_unpad, out_unpad, softmax_ls
 # ----------------------------------------------------------------------------------------------
 def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.95, min_keep=1,
                  max_keep=1, force_tail=0, scale=None, mask_count=None, want_mask=True,
-                 staged_event=None, rand=None, philox=None, pool=None, pyr=None, level=None):
+                 staged_event=None, rand=None, philox=None, pool=None, pyr=None, level=None,
+                 rows_kept=None):
     """vb_mask_predict. q,k [B,H,L,D]; q_off/k_off int32 [B,H,32]. Returns (po, mask) with
     po [B,H,nb,nb] in q.dtype and mask uint8 [B,H,nb,nb] (None with want_mask=False: the scores
     only, no energy rule). ``staged_event`` (a torch.cuda.Event) is recorded once the sampled
@@ -314,12 +328,14 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
     ``pyr=(v, outs)``: the multi-level KV pyramid pass (vb_kv_pyramid of k, v through ``rows``)
     run the same way; ``outs`` = kv_pyramid_outputs(k). Excludes ``pool``.
     ``level=mask_ratios``: the returned mask is the multi-level rank-band mask (level_mask's rule
-    on the scores, computed by the score kernel's epilogue) instead of the energy mask."""
+    on the scores, computed by the score kernel's epilogue) instead of the energy mask.
+    ``rows_kept``: int32 [B,H,nb] receiving the energy rule's kept-block count per mask row."""
     try:
         return _mask_predict(q, k, q_off, k_off, rows=rows, energy_threshold=energy_threshold,
                              min_keep=min_keep, max_keep=max_keep, force_tail=force_tail, scale=scale,
                              mask_count=mask_count, want_mask=want_mask, staged_event=staged_event,
-                             rand=rand, philox=philox, pool=pool, pyr=pyr, level=level)
+                             rand=rand, philox=philox, pool=pool, pyr=pyr, level=level,
+                             rows_kept=rows_kept)
     except Exception as e:
         # the claimed draws go back to the generator only when nothing was launched: a Python-side
         # validation error, or the library refusing the call (VB_ERR_INVALID / _UNSUPPORTED, raised
@@ -333,7 +349,7 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
 
 
 def _mask_predict(q, k, q_off, k_off, *, rows, energy_threshold, min_keep, max_keep, force_tail,
-                  scale, mask_count, want_mask, staged_event, rand, philox, pool, pyr, level):
+                  scale, mask_count, want_mask, staged_event, rand, philox, pool, pyr, level, rows_kept):
     if k.shape != q.shape:
         raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
                          f"got k {tuple(k.shape)}")
@@ -404,6 +420,10 @@ def _mask_predict(q, k, q_off, k_off, *, rows, energy_threshold, min_keep, max_k
         a.mask_level, a.level_bands = 1, len(vals)
         a.level_band_value, a.level_band_start, a.level_band_end = (
             vals.ctypes.data, st.ctypes.data, en.ctypes.data)
+    if rows_kept is not None:
+        if rows_kept.dtype != torch.int32 or rows_kept.numel() != B * H * nb or not rows_kept.is_contiguous():
+            raise ValueError("mask_predict: rows_kept must be contiguous int32 [B,H,nb]")
+        a.mask_rows_kept = rows_kept.data_ptr()
     check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
 
