@@ -34,10 +34,12 @@
 #define VB_KV64_WAVES 1    // waves per SIMD the D=64 kernel is register-budgeted for (2 spills)
 #endif
 #ifndef VB_BWD_DQ128_DEFAULT
-#define VB_BWD_DQ128_DEFAULT 0
+#define VB_BWD_DQ128_DEFAULT 1
 #endif
 #ifndef VB_BWD_DQ128_RING
-#define VB_BWD_DQ128_RING 4  // ring slots of the D=128 dQ pipeline: 4, or 2 (two workgroups per CU)
+// ring slots of the D=128 dQ pipeline: 2 (two workgroups per CU; Wan backward 1.073x over the
+// round-3 dQ, 1.057x over the 4-slot form, profiles/r05_bwd_dq2_ab.log) or 4 (one per CU)
+#define VB_BWD_DQ128_RING 2
 #endif
 #ifndef VB_DQ2_LA
 #define VB_DQ2_LA 2        // operand lookahead of the 2-slot dQ pipeline
