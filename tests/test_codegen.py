@@ -87,7 +87,7 @@ KV128_KERNELS = ([f"_ZN2vb20bwd_dkdv_pipe_kernelILi{d}ENS_{t}ELb{p}EEEvNS_9BwdPa
                   for d in (64, 128) for t in ("4BF16", "3F16") for p in (0, 1)] +
                  # dQ: <D, T, pooled, ring slots R> (R = 2: the two-workgroups-per-CU D=128 form)
                  [f"_ZN2vb18bwd_dq_pipe_kernelILi{d}ENS_{t}ELb{p}ELi{r}EEEvNS_9BwdParamsE"
-                  for d, r in ((64, 4), (128, 4), (128, 2)) for t in ("4BF16", "3F16") for p in (0, 1)])
+                  for d, r in ((64, 4), (64, 2), (128, 4), (128, 2)) for t in ("4BF16", "3F16") for p in (0, 1)])
 
 
 @pytest.fixture(scope="module")

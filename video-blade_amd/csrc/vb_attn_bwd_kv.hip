@@ -44,6 +44,14 @@
 #ifndef VB_DQ2_LA
 #define VB_DQ2_LA 2        // operand lookahead of the 2-slot dQ pipeline
 #endif
+#ifndef VB_BWD_DQ64_RING
+// ring slots of the D=64 dQ pipeline: 2 (CogVideoX backward 1.011x over 4, bit-for-bit the same
+// math as the D=128 form; profiles/r05_bwd_dq64_ring_ab.log) or 4
+#define VB_BWD_DQ64_RING 2
+#endif
+#ifndef VB_DQ64_R2_WGS
+#define VB_DQ64_R2_WGS 2     // workgroups per CU the D=64 2-slot form is register-budgeted for (3: 1.005x)
+#endif
 #ifndef VB_BWD_DQ64_DEFAULT
 #define VB_BWD_DQ64_DEFAULT 1
 #endif
@@ -862,7 +870,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
 // R = 4: the 4-slot ring (one workgroup per CU at D=128); R = 2: the 2-slot ring with half-tile DMA
 // batches, two workgroups per CU (QSched)
 template <int D, class T, bool kPool, int R>
-__global__ void __launch_bounds__(bwd::kThreads, R == 2 ? 2 : (D == 128 ? 1 : VB_KV64_WAVES))
+__global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ64_R2_WGS) : (D == 128 ? 1 : VB_KV64_WAVES))
     bwd_dq_pipe_kernel(const BwdParams p) {
   using namespace bwd;
   using namespace kvp;
@@ -1362,7 +1370,7 @@ static int dq128_ring() {
 }
 
 int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s) {
-  if (D == 64) return launch_dq<64, 4>(p, pool, f16, s);
+  if (D == 64) return VB_BWD_DQ64_RING == 2 ? launch_dq<64, 2>(p, pool, f16, s) : launch_dq<64, 4>(p, pool, f16, s);
   return dq128_ring() == 2 ? launch_dq<128, 2>(p, pool, f16, s) : launch_dq<128, 4>(p, pool, f16, s);
 }
 
