@@ -83,11 +83,17 @@ def test_makefile_falls_back_when_the_scheduler_option_is_gone():
 # miscounted wait, would read stale data. tools/diag/lgkm_check.py models the LDS counter over the
 # ISA and reports any such use.
 KV128_SRC = os.path.join(ROOT, "video-blade_amd", "csrc", "vb_attn_bwd_kv.hip")
-KV128_KERNELS = ([f"_ZN2vb20bwd_dkdv_pipe_kernelILi{d}ENS_{t}ELb{p}EEEvNS_9BwdParamsE"
+KV128_KERNELS = ([f"_ZN2vb20bwd_dkdv_pipe_kernelILi{d}ENS_{t}ELb{p}ELb0EEEvNS_9BwdParamsE"
                   for d in (64, 128) for t in ("4BF16", "3F16") for p in (0, 1)] +
+                 # the multi-level level-1 dK/dV
+                 [f"_ZN2vb20bwd_dkdv_pipe_kernelILi{d}ENS_{t}ELb0ELb1EEEvNS_9BwdParamsE"
+                  for d in (64, 128) for t in ("4BF16", "3F16")] +
                  # dQ: <D, T, pooled, ring slots R> (R = 2: the two-workgroups-per-CU D=128 form)
-                 [f"_ZN2vb18bwd_dq_pipe_kernelILi{d}ENS_{t}ELb{p}ELi{r}EEEvNS_9BwdParamsE"
-                  for d, r in ((64, 4), (64, 2), (128, 4), (128, 2)) for t in ("4BF16", "3F16") for p in (0, 1)])
+                 [f"_ZN2vb18bwd_dq_pipe_kernelILi{d}ENS_{t}ELb{p}ELi{r}ELb0EEEvNS_9BwdParamsE"
+                  for d, r in ((64, 4), (64, 2), (128, 4), (128, 2)) for t in ("4BF16", "3F16") for p in (0, 1)] +
+                 # the multi-level dQ (2-slot ring, no pooled branch)
+                 [f"_ZN2vb18bwd_dq_pipe_kernelILi{d}ENS_{t}ELb0ELi2ELb1EEEvNS_9BwdParamsE"
+                  for d in (64, 128) for t in ("4BF16", "3F16")])
 
 
 @pytest.fixture(scope="module")
@@ -153,7 +159,8 @@ def test_pipeline_tiles_have_no_per_piece_branches(kv128_asm, name):
             br += 1
     steady = [b for m, b in windows if m >= 8]   # windows of the tile loop
     assert steady, "no tile windows found in " + name
-    limit = 4 if "dq_pipe" in name and "ELb1ELi" in name else 1
+    # the pooled dQ's switch to the pooled seeds, the multi-level dQ's per-level bias switches
+    limit = 4 if "dq_pipe" in name and ("ELb1ELi" in name or "ELi2ELb1E" in name) else 1
     assert max(steady) <= limit, (name, sorted(set(steady)))
 
 

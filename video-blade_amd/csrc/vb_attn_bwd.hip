@@ -1303,8 +1303,13 @@ static int launch_ml_grads(const PrepParams& pp, const BwdParams& p, hipStream_t
   const int BH = p.B * p.H;
   hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true, true>), dim3(p.nbkp * BH), dim3(bwd::kThreads), 0, s, p);
   if (int rc = check_launch("bwd_dkdv_kernel<multi-level pooled>")) return rc;
-  hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, false, true>), dim3(p.nbk * BH), dim3(bwd::kThreads), 0, s, p);
-  if (int rc = check_launch("bwd_dkdv_kernel<multi-level>")) return rc;
+  if (ml_dkdv_pipe_enabled()) {
+    if (int rc = launch_ml_dkdv_pipe(p, D, std::is_same<T, F16>::value, s)) return rc;
+  } else {
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, false, true>), dim3(p.nbk * BH), dim3(bwd::kThreads), 0, s, p);
+    if (int rc = check_launch("bwd_dkdv_kernel<multi-level>")) return rc;
+  }
+  if (ml_dq_pipe_enabled()) return launch_ml_dq_pipe(p, D, std::is_same<T, F16>::value, s);
   hipLaunchKernelGGL((bwd_dq_kernel<D, T, false, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
   return check_launch("bwd_dq_kernel<multi-level>");
 }

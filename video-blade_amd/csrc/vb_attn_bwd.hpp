@@ -72,6 +72,12 @@ int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream
 bool dkdv_pipe_enabled(int D);
 // the hand-scheduled dQ kernels (same file; grid nbq * B*H), env VB_BWD_DQ128 / VB_BWD_DQ64
 int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s);
+// the multi-level dQ on the 2-slot pipeline (vb_ml_attn_bwd); ml_dq_pipe_enabled() reads VB_BWD_MLDQ once
+int launch_ml_dq_pipe(const BwdParams& p, int D, bool f16, hipStream_t s);
+bool ml_dq_pipe_enabled();
+// the multi-level level-1 dK/dV on the pipeline kernel (VB_BWD_MLKV, read once)
+int launch_ml_dkdv_pipe(const BwdParams& p, int D, bool f16, hipStream_t s);
+bool ml_dkdv_pipe_enabled();
 bool dq_pipe_enabled(int D);
 
 }  // namespace vb

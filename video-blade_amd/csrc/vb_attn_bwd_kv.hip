@@ -203,6 +203,11 @@ __device__ __forceinline__ void rdtr(s16x4& r, uint32_t addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(kImm));
 #endif
 }
+__device__ __forceinline__ void rd64(u32x2& r, uint32_t addr) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(addr));
+#endif
+}
 __device__ __forceinline__ void rdu16(uint32_t& r, uint32_t addr) {
 #if __HIP_DEVICE_COMPILE__
   asm volatile("ds_read_u16 %0, %1" : "=v"(r) : "v"(addr));
@@ -384,11 +389,16 @@ __device__ __forceinline__ void qgap(f32x16& s, f32x16& dp, u32x4 (&pd)[2], floa
 
 }  // namespace kvp
 
-// D=128: one workgroup per CU (one wave per SIMD); D=64: VB_KV64_WAVES
-template <int D, class T, bool kPooled>
+// D=128: one workgroup per CU (one wave per SIMD); D=64: VB_KV64_WAVES.
+// kML: the multi-level backward's level-1 dK/dV (vb_ml_attn_bwd; bwd_dkdv_kernel<kPooled = false,
+// kML>): K/V are the pyramids' level-1 rows, a key block takes the q-blocks whose level for it is 1,
+// and each key adds the mean-pool adjoints of its level-2/4/8 pyramid rows (the reference kernel's
+// _bwd_kv epilogue, block_sparse_attn_kernel_with_backward_9_10.py:1494-1563).
+template <int D, class T, bool kPooled, bool kML = false>
 __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) bwd_dkdv_pipe_kernel(const BwdParams p) {
   using namespace bwd;
   using namespace kvp;
+  static_assert(!(kML && kPooled), "the multi-level pooled levels run bwd_dkdv_kernel's union walk");
   using S = Sched<D>;
   using V8 = typename T::vec8;
   constexpr int KS = S::KS, DT = S::DT, RB = S::RB, N = S::N, kSec = S::kSec, TB = S::kTileBytes;
@@ -414,7 +424,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
     bh = lin / nkb;
     kblk = lin % nkb;
   } else {
-    const int hr = min(p.heavy_rows, nkb);
+    const int hr = kML ? 0 : min(p.heavy_rows, nkb);
     const int n_heavy = hr * BH;
     if ((int)blockIdx.x < n_heavy) {
       kblk = nkb - 1 - (int)(blockIdx.x / BH);
@@ -471,7 +481,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
 #pragma unroll
     for (int r = 0; r < kCPW; ++r) {
       const int i = qlo + 64 * (wave + 4 * r) + lane;
-      const bool keep = (i < qhi) && (mcol == nullptr || mcol[(int64_t)i * p.ms[2]] != 0);
+      const bool keep = (i < qhi) && (mcol == nullptr || (kML ? mcol[(int64_t)i * p.ms[2]] == 1 : mcol[(int64_t)i * p.ms[2]] != 0));
       bal[r] = __ballot(keep);
       if (lane == 0) chunk_n[wave + 4 * r] = __popcll(bal[r]);
     }
@@ -813,6 +823,49 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
       }
     return;
   }
+  if constexpr (kML) {   // level-1 key: + the mean-pool adjoints of its level-2/4/8 pyramid rows
+    const int64_t rb = (int64_t)bh * (7 * (p.Lpad / 8));
+    const float* qk[3];
+    const float* qv[3];
+#pragma unroll
+    for (int e = 1; e < 4; ++e) {
+      const int64_t row = rb + (MlGeom(p.Lpad).off[e] - p.Lpad) + (key >> e);
+      qk[e - 1] = p.dkpyr + row * D;
+      qv[e - 1] = p.dvpyr + row * D;
+    }
+    const int64_t orow = p.kv_rows ? p.kv_rows[key] : krow0 + key;
+    uint8_t* dkr = reinterpret_cast<uint8_t*>(p.dk) + 2 * (b * p.dks[0] + h * p.dks[1] + orow * p.dks[2]);
+    uint8_t* dvr = reinterpret_cast<uint8_t*>(p.dv) + 2 * (b * p.dvs[0] + h * p.dvs[1] + orow * p.dvs[2]);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * half;
+        float a[4], cc[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = dk[dt][4 * g4 + e] * p.scale;
+          cc[e] = dv[dt][4 * g4 + e];
+        }
+#pragma unroll
+        for (int lv = 0; lv < 3; ++lv) {
+          const float w = 1.0f / (float)(2 << lv);
+          const f32x4 x = *reinterpret_cast<const f32x4*>(qk[lv] + d);
+          const f32x4 y = *reinterpret_cast<const f32x4*>(qv[lv] + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] = fmaf(x[e], w, a[e]);
+            cc[e] = fmaf(y[e], w, cc[e]);
+          }
+        }
+        u32x2 w2, z;
+        w2[0] = pack2<T>(a[0], a[1]); w2[1] = pack2<T>(a[2], a[3]);
+        z[0] = pack2<T>(cc[0], cc[1]); z[1] = pack2<T>(cc[2], cc[3]);
+        *reinterpret_cast<u32x2*>(dkr + d * 2) = w2;
+        *reinterpret_cast<u32x2*>(dvr + d * 2) = z;
+      }
+    return;
+  }
   // full-resolution key: + mean-pool adjoint of the pooled grads (replicate padding folds onto
   // the last token), written at the caller's row
   const float* pk = nullptr;
@@ -868,19 +921,29 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_KV64_WAVES) b
 // nothing to dQ (dQ^T += K^T.dS^T with K = 0).
 // ------------------------------------------------------------------------------------------------
 // R = 4: the 4-slot ring (one workgroup per CU at D=128); R = 2: the 2-slot ring with half-tile DMA
-// batches, two workgroups per CU (QSched)
-template <int D, class T, bool kPool, int R>
-__global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ64_R2_WGS) : (D == 128 ? 1 : VB_KV64_WAVES))
+// batches, two workgroups per CU (QSched).
+// kML: the multi-level backward's dQ (vb_ml_attn_bwd; the reference kernel's _bwd_dq pass,
+// block_sparse_attn_kernel_with_backward_9_10.py:1420-1505): K/V are the pyramids, and the tiles are
+// bwd_dq_kernel<kML>'s: level 1 (two per kept block), one per level-2 block, two level-4 blocks and
+// four level-8 blocks per tile, each tile carrying its level's +log2(p) logit bias. A tile's four
+// 16-row quarters come from a per-tile table built in the prologue; a quarter past its level's list
+// and level-1 keys past L (without ref_tail) read as zero rows.
+template <int D, class T, bool kPool, int R, bool kML = false>
+__global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? (kML ? 1 : 2) : VB_DQ64_R2_WGS) : (D == 128 ? 1 : VB_KV64_WAVES))
     bwd_dq_pipe_kernel(const BwdParams p) {
   using namespace bwd;
   using namespace kvp;
   using S = QSched<D, R, R == 2 ? VB_DQ2_LA : kLA>;
   using V8 = typename T::vec8;
+  static_assert(!kML || (R == 2 && !kPool), "the multi-level dQ runs on the 2-slot ring, no pooled branch");
   constexpr int KS = S::KS, DT = S::DT, RB = S::RB, N = S::N, TB = S::kTileBytes;
   constexpr int kPieces = S::kPieces, kPQ = S::kPQ;
   constexpr int kLA = S::LA;              // shadows kvp::kLA
   constexpr bool kSeeded = R == 4;        // R = 2 holds no -Delta seed tile (qop)
-  __shared__ __attribute__((aligned(16))) uint8_t smem[S::kLdsBytes];
+  // multi-level: per tile, its four quarters' pyramid rows / 16 (u16; 0xFFFF = a zero quarter)
+  constexpr int kMlTiles = 2 * kMaxBlocks + kMaxBlocks + kMaxBlocks / 2 + kMaxBlocks / 4 + 8;
+  constexpr int kTabOff = (S::kLdsBytes + 7) / 8 * 8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kML ? kTabOff + 8 * kMlTiles : S::kLdsBytes];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + S::kListOff);
   int* list_n = reinterpret_cast<int*>(smem + S::kListOff + 2 * kMaxBlocks);   // [4] + chunk counts
 
@@ -939,8 +1002,35 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
       qf[s] = *reinterpret_cast<const V8*>(qp + (16 * s + 8 * half) * 2);
       df[s] = *reinterpret_cast<const V8*>(dp_ + (16 * s + 8 * half) * 2);
     }
-    {   // the kept key blocks, ascending: the four waves ballot 64-block chunks wave, wave + 4, .. in
-        // one round of mask loads, then place their entries after the counts of the chunks before them
+    if constexpr (kML) {   // per-level key-block lists, levels 1, 2, 4, 8 in that order (wave 0)
+      if (wave == 0) {
+        int cnt[4] = {0, 0, 0, 0};
+        for (int j0 = 0; j0 < nbk; j0 += 64) {
+          const int j = j0 + lane;
+          const int lv = j < nbk ? mrow[j] : 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cnt[e] += __popcll(__ballot(lv == (1 << e)));
+        }
+        int pos[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+        for (int j0 = 0; j0 < nbk; j0 += 64) {
+          const int j = j0 + lane;
+          const int lv = j < nbk ? mrow[j] : 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const unsigned long long bal = __ballot(lv == (1 << e));
+            if (lv == (1 << e))
+              list[pos[e] + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
+                  (uint16_t)j;
+            pos[e] += __popcll(bal);
+          }
+#if __HIP_DEVICE_COMPILE__
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // a bounded LDS-counter state per iteration (lgkm_check)
+#endif
+        }
+        if (lane < 4) list_n[lane] = lane == 0 ? cnt[0] : lane == 1 ? cnt[1] : lane == 2 ? cnt[2] : cnt[3];
+      }
+    } else {   // the kept key blocks, ascending: the four waves ballot 64-block chunks wave, wave + 4, .. in
+               // one round of mask loads, then place their entries after the counts of the chunks before them
       constexpr int kCPW = kMaxBlocks / 64 / 4;
       int* chunk_n = list_n + 4;
       unsigned long long bal[kCPW];
@@ -977,9 +1067,44 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
   __syncthreads();
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
   int ntm = 2 * nkept;
-  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kBlk + kT >= Lk) ntm -= 1;
+  if (nkept > 0 && list[nkept - 1] == nbk - 1 && (nbk - 1) * kBlk + kT >= Lk && !(kML && p.ref_tail)) ntm -= 1;
   const int ntp = kPool ? (p.Lkp + kT - 1) / kT : 0;
-  const int ntiles = ntm + ntp;
+  // multi-level tile ranges: [0, ntm) level 1, [ntm, T12) level 2, [T12, T124) level 4, then level 8
+  int T12 = ntm, T124 = ntm, ntiles = ntm + ntp;
+  if constexpr (kML) {
+    const int n2 = __builtin_amdgcn_readfirstlane(list_n[1]);
+    const int n4 = __builtin_amdgcn_readfirstlane(list_n[2]);
+    const int n8 = __builtin_amdgcn_readfirstlane(list_n[3]);
+    T12 = ntm + n2;
+    T124 = T12 + (n4 + 1) / 2;
+    ntiles = T124 + (n8 + 3) / 4;
+    // the quarter table (bwd_dq_kernel<kML>'s ml_quarter, rows / 16; zero quarters past a list)
+    const int r2 = p.Lpad / 16, r4 = r2 + p.Lpad / 32, r8 = r4 + p.Lpad / 64;
+    uint32_t* tab = reinterpret_cast<uint32_t*>(smem + kTabOff);
+    // branch-free per entry (selects): one list read per quarter
+    for (int tt = threadIdx.x; tt < ntiles; tt += kThreads) {
+      const int lv = (tt >= ntm) + (tt >= T12) + (tt >= T124);
+      uint32_t w[2] = {0u, 0u};
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const int e = lv == 2 ? 2 * (tt - T12) + (qd >> 1) : 4 * (tt - T124) + qd;   // levels 4, 8
+        const int li = lv == 0 ? tt >> 1 : lv == 1 ? nkept + tt - ntm : lv == 2 ? nkept + n2 + e : nkept + n2 + n4 + e;
+        const bool ok = lv < 2 || e < (lv == 2 ? n4 : n8);
+        const int blk = (int)list[max(min(li, kMaxBlocks - 1), 0)];
+        const int r16 = lv == 0 ? blk * 8 + (tt & 1) * 4 + qd
+                      : lv == 1 ? r2 + blk * 4 + qd
+                      : lv == 2 ? r4 + blk * 2 + (qd & 1)
+                                : r8 + blk;
+        w[qd >> 1] |= (uint32_t)(ok ? r16 : 0xFFFF) << (16 * (qd & 1));
+      }
+      tab[2 * tt] = w[0];
+      tab[2 * tt + 1] = w[1];
+#if __HIP_DEVICE_COMPILE__
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // a bounded LDS-counter state per iteration (lgkm_check)
+#endif
+    }
+    __syncthreads();
+  }
 
   f32x16 dq[DT];
 #pragma unroll
@@ -1004,6 +1129,8 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
     // the lane's voffset per key source (main / pooled row strides). R = 2 keeps piece 0's only:
     // the swizzle depends on row bits the piece index does not touch (rows differ by 4 kRpp k), so
     // piece k adds 4 kRpp k rows as a scalar offset (TileDma::krb / vrb)
+    // Multi-level: a piece's rows lie in one 16-row quarter (pieces start at multiples of kRpp),
+    // so its voffset is the row within the quarter and the quarter's pyramid row the soffset.
     constexpr int kVo = R == 2 ? 2 : kPieces;
     int voff_m[kVo], voff_p[kVo];
 #pragma unroll
@@ -1011,7 +1138,7 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
       const bool isv = R == 2 ? k == 1 : k >= kPQ;
       const int r = (wave + 4 * (R == 2 ? 0 : k % kPQ)) * S::kRpp + lane / (RB / 16);
       const int c16 = 16 * ((lane % (RB / 16)) ^ dual_swz<D>(r));
-      voff_m[k] = r * (isv ? vrowb : krowb) + c16;
+      voff_m[k] = (kML ? (r & 15) : r) * (isv ? vrowb : krowb) + c16;
       voff_p[k] = r * (isv ? vprowb : kprowb) + c16;
     }
     struct TileDma {
@@ -1019,6 +1146,7 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
       int soff_k, soff_v;
       int krb, vrb;   // row strides (R = 2)
       bool pooled;
+      int qk[4], qv[4];   // multi-level: the quarters' byte offsets (K, V)
     };
     // tile tt's source: kept block list[tt/2] half tt%2, then pooled tiles; past the end zero-extent
     // Every select below takes opaque operands (readfirstlane / an empty asm): hipcc otherwise turns
@@ -1059,8 +1187,47 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
       d.soff_v = kstart * d.vrb;
       return d;
     };
+    // multi-level tile tt from its table entry (w0 = quarters 0-1, w1 = 2-3, rows / 16): level-1
+    // tiles end at L unless ref_tail (zero rows past it), the other levels at the pyramid's end
+    const int ml_kall = kML ? (int)((int64_t)(15 * (p.Lpad / 8) - 1) * krowb + RB) : 0;
+    const int ml_vall = kML ? (int)((int64_t)(15 * (p.Lpad / 8) - 1) * vrowb + RB) : 0;
+    auto tile_dma_ml = [&](int tt, uint32_t w0, uint32_t w1) __attribute__((always_inline)) -> TileDma {
+      TileDma d{};
+      const int lm = -(int)(tt < ntiles);
+      const bool l1 = tt < ntm && !p.ref_tail;
+      d.k = srd_t{reinterpret_cast<const void*>(((uint64_t)sm.khi << 32) | sm.klo), (l1 ? sm.kbytes : uniform(ml_kall)) & lm};
+      d.v = srd_t{reinterpret_cast<const void*>(((uint64_t)sm.vhi << 32) | sm.vlo), (l1 ? sm.vbytes : uniform(ml_vall)) & lm};
+      d.krb = krowb;
+      d.vrb = vrowb;
+      const int q16[4] = {(int)(w0 & 0xFFFF), (int)(w0 >> 16), (int)(w1 & 0xFFFF), (int)(w1 >> 16)};
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        d.qk[qd] = q16[qd] * 16 * krowb;
+        d.qv[qd] = q16[qd] * 16 * vrowb;
+      }
+      return d;
+    };
     auto piece = [&](const TileDma& d, int slot, int k) __attribute__((always_inline)) {
       const int kv = R == 2 ? (k >= kPQ) : k;
+      if constexpr (kML) {
+        // the piece's quarter: (kRpp (wave + 4 kk)) / 16 = q0 + (kRpp wave) / 16 with q0 known here
+        // and the wave part 0 (D=128) or wave / 2 (D=64), blended with a uniform mask (a select
+        // between the two fields would become an indexed load from scratch)
+        const int kk = k < kPQ ? k : k - kPQ;
+        const int q0 = (S::kRpp * 4 * kk) >> 4;
+        int sk = d.qk[q0], sv = d.qv[q0];
+        if constexpr (S::kRpp * 3 >= 16) {
+          int wm = uniform(-(((S::kRpp * wave) >> 4) & 1));
+#if __HIP_DEVICE_COMPILE__
+          asm volatile("" : "+s"(wm));
+#endif
+          sk = (sk & ~wm) | (d.qk[(q0 + 1) & 3] & wm);
+          sv = (sv & ~wm) | (d.qv[(q0 + 1) & 3] & wm);
+        }
+        if (k < kPQ) dma16(d.k, smem + S::kKOff + slot * TB + (wave + 4 * k) * 1024, voff_m[kv], sk);
+        else dma16(d.v, smem + S::kVOff + slot * TB + (wave + 4 * kk) * 1024, voff_m[kv], sv);
+        return;
+      }
       int vo = voff_m[kv];
       if constexpr (kPool) {   // one v_bfi on a uniform mask; a select here becomes a branch per piece
         int pm = uniform(d.pooled ? -1 : 0);
@@ -1081,6 +1248,15 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
     };
     auto list_at = [&](int tt) __attribute__((always_inline)) -> int {
       return __builtin_amdgcn_readfirstlane((int)list[max(min(tt >> 1, nkept - 1), 0)]);
+    };
+    const uint32_t* tab32 = reinterpret_cast<const uint32_t*>(smem + kTabOff);
+    auto tile_at = [&](int tt) __attribute__((always_inline)) -> TileDma {
+      if constexpr (kML) {
+        const int i = min(tt, kMlTiles - 1);
+        return tile_dma_ml(tt, (uint32_t)uniform((int)tab32[2 * i]), (uint32_t)uniform((int)tab32[2 * i + 1]));
+      } else {
+        return tile_dma(tt, list_at(tt));
+      }
     };
 
     const uint32_t sbase = static_cast<uint32_t>(
@@ -1114,7 +1290,20 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
     u32x4 pd0[2], pd1[2];
     V8 nx[kLA];
     uint32_t blk_raw = 0;
+    u32x2 tab_raw = {0u, 0u};
+    const uint32_t taba = sbase + kTabOff;
     TileDma dn{};
+    // multi-level: the tile's level exponent e (0..3) is its logit bias +log2(2^e) = e
+    auto ml_level = [&](int tt) __attribute__((always_inline)) -> int {
+      return tt < ntm ? 0 : tt < T12 ? 1 : tt < T124 ? 2 : 3;
+    };
+    auto set_level = [&](int e) __attribute__((always_inline)) {
+      nd0 = opaque(D1);
+      nl0 = (float)e - opaque(L1);
+    };
+    auto ml_level_s = [&](int tt) __attribute__((always_inline)) -> int {   // scalar selects, no branches
+      return (int)(tt >= ntm) + (int)(tt >= T12) + (int)(tt >= T124);
+    };
     auto set_class = [&](bool pooled) __attribute__((always_inline)) {
       const float dr = pooled ? opaque(D2) : opaque(D1);
       if constexpr (kSeeded) {
@@ -1142,12 +1331,12 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
     } else {
       // ---- prologue: both halves of tile 0 in flight, half 0 landed; dn = tile 1 (its halves
       // are issued in tile 0, at gaps kP0.. and after G1) ---------------------------------------
-      dn = tile_dma(0, list_at(0));
+      dn = tile_at(0);
 #pragma unroll
       for (int j = 0; j < S::kHalf; ++j) half_piece(dn, 0, 0, j);
 #pragma unroll
       for (int j = 0; j < S::kHalf; ++j) half_piece(dn, 0, 1, j);
-      dn = tile_dma(1, list_at(1));
+      dn = tile_at(1);
       VB_WAIT_VMCNT(S::kHalf);
     }
     __builtin_amdgcn_s_barrier();
@@ -1161,7 +1350,8 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
 #endif
 #pragma unroll
     for (int q = 0; q < kLA; ++q) launder(nx[q]);
-    set_class(kPool && 0 >= ntm);
+    if constexpr (kML) set_level(ml_level(0));
+    else set_class(kPool && 0 >= ntm);
 
     auto iter = [&](int t, auto U, auto M) __attribute__((always_inline)) {
       constexpr int u = decltype(U)::value % R;   // tile t's ring slot (t mod R)
@@ -1211,8 +1401,13 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
         if constexpr (R == 2 && mode != 2 && g == S::kG1) half_barrier();
         if constexpr (R == 2 && mode != 2 && g == S::kG2) {
           half_barrier();
-          launder(blk_raw);
-          dn = tile_dma(t + 2, __builtin_amdgcn_readfirstlane((int)blk_raw));   // for tile t+1's batches
+          if constexpr (kML) {
+            launder(tab_raw);
+            dn = tile_dma_ml(t + 2, (uint32_t)uniform((int)tab_raw[0]), (uint32_t)uniform((int)tab_raw[1]));
+          } else {
+            launder(blk_raw);
+            dn = tile_dma(t + 2, __builtin_amdgcn_readfirstlane((int)blk_raw));   // for tile t+1's batches
+          }
         }
         // ---- fillers of gap g ----
         constexpr int m = g + kLA;
@@ -1230,7 +1425,10 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
             rdtr<imm>(yhi[m], ya[dt][1]);
           }
         }
-        if constexpr (g == S::kList) rdu16(blk_raw, lista + 2 * max(min((t + (R == 4 ? 3 : 2)) >> 1, nkept - 1), 0));
+        if constexpr (g == S::kList) {
+          if constexpr (kML) rd64(tab_raw, taba + 8 * min(t + 2, kMlTiles - 1));
+          else rdu16(blk_raw, lista + 2 * max(min((t + (R == 4 ? 3 : 2)) >> 1, nkept - 1), 0));
+        }
         if constexpr (g >= S::kNx && g < S::kNx + kLA) {
           constexpr int q = g - S::kNx;
           rd128<un * TB + ((q & 1) ? kVImm : 0)>(nx[q], xa[(q & 1) && !kShare][q >> 1]);
@@ -1262,10 +1460,12 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? 2 : VB_DQ6
         if constexpr (g == N - 1) {
 #pragma unroll
           for (int q = 0; q < kLA; ++q) launder(nx[q]);
-          // tile t+1's seeds and -L': they change once, at the first pooled tile
+          // tile t+1's seeds and -L': they change once, at the first pooled tile (multi-level: at
+          // each level's first tile)
           if constexpr (mode != 2 && kPool) {
             if (t + 1 == ntm) set_class(true);
           }
+          if constexpr (mode != 2 && kML) set_level(ml_level_s(t + 1));   // every tile: two VALU
         }
         __builtin_amdgcn_sched_barrier(0);
       };
@@ -1372,6 +1572,44 @@ static int dq128_ring() {
 int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s) {
   if (D == 64) return VB_BWD_DQ64_RING == 2 ? launch_dq<64, 2>(p, pool, f16, s) : launch_dq<64, 4>(p, pool, f16, s);
   return dq128_ring() == 2 ? launch_dq<128, 2>(p, pool, f16, s) : launch_dq<128, 4>(p, pool, f16, s);
+}
+
+#ifndef VB_BWD_MLDQ_DEFAULT
+#define VB_BWD_MLDQ_DEFAULT 1
+#endif
+bool ml_dq_pipe_enabled() {
+  static const bool on = env_switch("VB_BWD_MLDQ", VB_BWD_MLDQ_DEFAULT);
+  return on;
+}
+#ifndef VB_BWD_MLKV_DEFAULT
+#define VB_BWD_MLKV_DEFAULT 1
+#endif
+bool ml_dkdv_pipe_enabled() {
+  static const bool on = env_switch("VB_BWD_MLKV", VB_BWD_MLKV_DEFAULT);
+  return on;
+}
+int launch_ml_dkdv_pipe(const BwdParams& p, int D, bool f16, hipStream_t s) {
+  const dim3 grid(p.nbk * p.B * p.H);
+  if (D == 128) {
+    if (f16) hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<128, F16, false, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<128, BF16, false, true>), grid, dim3(bwd::kThreads), 0, s, p);
+  } else {
+    if (f16) hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<64, F16, false, true>), grid, dim3(bwd::kThreads), 0, s, p);
+    else hipLaunchKernelGGL((bwd_dkdv_pipe_kernel<64, BF16, false, true>), grid, dim3(bwd::kThreads), 0, s, p);
+  }
+  return check_launch("bwd_dkdv_pipe_kernel<multi-level>");
+}
+
+template <int D>
+static int launch_ml_dq(const BwdParams& p, bool f16, hipStream_t s) {
+  const dim3 grid(p.nbq * p.B * p.H);
+  if (f16) hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, F16, false, 2, true>), grid, dim3(bwd::kThreads), 0, s, p);
+  else hipLaunchKernelGGL((bwd_dq_pipe_kernel<D, BF16, false, 2, true>), grid, dim3(bwd::kThreads), 0, s, p);
+  return check_launch("bwd_dq_pipe_kernel<multi-level>");
+}
+
+int launch_ml_dq_pipe(const BwdParams& p, int D, bool f16, hipStream_t s) {
+  return D == 128 ? launch_ml_dq<128>(p, f16, s) : launch_ml_dq<64>(p, f16, s);
 }
 
 int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream_t s) {
