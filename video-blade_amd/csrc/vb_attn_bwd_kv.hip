@@ -118,6 +118,8 @@ struct Sched {
   // and 0 .. kSec-1 of the next tile (before Y(t,1))
   static constexpr int kV0 = kSec + 2, kV0n = 2 * kSec - 2;
   static constexpr int kV1 = 3 * kSec + 2, kV1n = 2 * kSec - 2;
+  // (a barrier right after section B, the last reads of slot t-1, with tile t+3's pieces spread
+  // over the rest of the tile measured 1.00x / 0.99x, profiles/r05_bwd_dma_spread_ab.log)
   static constexpr int kGb = N - 12;                   // the tile barrier
   static constexpr int kDma0 = kGb > kV1 ? kGb : kV1;  // DMA pieces of tile t+3 from here (needs the list entry)
   static constexpr int kLq0 = kV0 - 10;                // L' of rows 0-31 (two gaps)
@@ -321,7 +323,8 @@ struct QSched {
   // R = 2
   static constexpr int kG1 = R == 2 ? kC - L : -1, kG2 = R == 2 ? N - L : -1;
   static constexpr int kHalf = kPieces / 2;                    // pieces per half-tile batch
-  static constexpr int kP0 = 0, kP1 = kG1 + 1;                 // first gaps of the two batches
+  static constexpr int kP0 = 0, kP1 = kG1 + 1;                 // first gaps of the two batches (back to
+                                                               // back; spread 3 or 5 gaps apart: 1.00x)
   static constexpr int kList = R == 4 ? kGb - 6 : kG2 - 4;     // the key block of tile t+3 (R=4) / t+2
   static constexpr int kNx = R == 4 ? kGb + 1 : kG2;           // tile t+1's first operands
   static_assert(R == 2 || kGb >= kC, "the barrier must follow the reads of the previous tile");
