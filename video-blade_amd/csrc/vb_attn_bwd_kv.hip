@@ -119,7 +119,7 @@ struct Sched {
   static constexpr int kV0 = kSec + 2, kV0n = 2 * kSec - 2;
   static constexpr int kV1 = 3 * kSec + 2, kV1n = 2 * kSec - 2;
   // (a barrier right after section B, the last reads of slot t-1, with tile t+3's pieces spread
-  // over the rest of the tile measured 1.00x / 0.99x, profiles/r05_bwd_dma_spread_ab.log)
+  // over the rest of the tile measured 1.00x / 0.99x, profiles/archive/r05_bwd_dma_spread_ab.log)
   static constexpr int kGb = N - 12;                   // the tile barrier
   static constexpr int kDma0 = kGb > kV1 ? kGb : kV1;  // DMA pieces of tile t+3 from here (needs the list entry)
   static constexpr int kLq0 = kV0 - 10;                // L' of rows 0-31 (two gaps)
