@@ -363,6 +363,31 @@ def test_longest_first_dispatch_order_is_bit_identical(variant, H, D):
         b = ops.attention_fwd(q, k_r, v_r, order=True, **kw)
         c = ops.attention_fwd(q, k_r, v_r, order=True, q_lengths=kept, **kw)
         assert torch.equal(a, b) and torch.equal(a, c)
+        # the permutation itself (attn_order_kernel), restated: per XCD range of the non-heavy
+        # rows, a permutation of the range whose (head, -kept) keys never decrease (equal keys may
+        # come in any order: the bins are filled with LDS atomics); with a window, the range's
+        # first count - window items keep their place
+        kc = kept.view(-1).cpu()
+        hr = min(m.force_tail, nb)
+        rows_left = nb - hr
+        nwg = rows_left * H
+        q8, r8 = nwg // 8, nwg % 8
+        for window in (0, 16):
+            qo = torch.full((H * nb,), -1, dtype=torch.int32, device=DEV)
+            ops.attention_fwd(q, k_r, v_r, order=True, q_lengths=kept, order_window=window, q_order_out=qo, **kw)
+            qo = qo.cpu()
+            for x in range(8):
+                start = x * (q8 + 1) if x < r8 else r8 * (q8 + 1) + (x - r8) * q8
+                count = q8 + (1 if x < r8 else 0)
+                skip = count - window if 0 < window < count else 0
+                seg = qo[start:start + count].tolist()
+                assert sorted(seg) == list(range(start, start + count)), (x, "not a permutation")
+                assert seg[:skip] == list(range(start, start + skip))
+                def key(lin):
+                    bh, qb = lin // rows_left, rows_left - 1 - lin % rows_left
+                    return (bh, -int(kc[bh * nb + qb]))
+                keys = [key(lin) for lin in seg[skip:]]
+                assert keys == sorted(keys), (x, "not longest first within each head")
 
 
 def test_sample_offsets_match_torch_topk_and_rng_order():

@@ -90,12 +90,14 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
                   vp: Optional[torch.Tensor] = None, kp_log_bias: float = 0.0, use_main: bool = True,
                   scale: Optional[float] = None, need_lse: bool = False,
                   out: Optional[torch.Tensor] = None, heavy_rows: int = 0, order: bool = False,
-                  q_lengths: Optional[torch.Tensor] = None, order_window: int = 0):
+                  q_lengths: Optional[torch.Tensor] = None, order_window: int = 0,
+                  q_order_out: Optional[torch.Tensor] = None):
     """vb_attn_fwd: softmax over (block-masked keys of k/v) ∪ (pooled keys kp/vp + bias).
     q,k,v [B,H,L,D]; block_mask [B,H,ceil(Lq/128),ceil(Lk/128)] bool/uint8; rows int32.
     ``order``: dispatch each XCD's q-blocks longest first (scheduling only; ``q_lengths`` [B,H,nbq]
     int32 kept blocks per mask row from mask_predict(rows_kept=...), else counted on the device;
-    ``order_window`` > 0 re-orders only the last that many q-blocks of each XCD's range).
+    ``order_window`` > 0 re-orders only the last that many q-blocks of each XCD's range;
+    ``q_order_out``: int32 [B*H*ceil(Lq/128)] to receive the dispatch permutation, for tests).
     Returns out [B,H,Lq,D] (and lse fp32 [B,H,Lq] when need_lse)."""
     dev = _require_gpu(q, k, v, block_mask, q_rows, kv_rows, kp, vp)
     q = _aligned_bhld(q)
@@ -143,7 +145,9 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
     a.heavy_rows = int(heavy_rows)
     if order and block_mask is not None and use_main:
         nbq = (Lq + BLOCK - 1) // BLOCK
-        q_order = torch.empty(B * H * nbq, device=dev, dtype=torch.int32)   # workspace
+        q_order = q_order_out if q_order_out is not None else torch.empty(B * H * nbq, device=dev, dtype=torch.int32)
+        if q_order.dtype != torch.int32 or q_order.numel() < B * H * nbq or not q_order.is_contiguous() or q_order.device != dev:
+            raise ValueError("attention_fwd: q_order_out must be a contiguous int32 tensor of B*H*ceil(Lq/128) on q's device")
         a.q_order = q_order.data_ptr()
         a.order_window = int(order_window)
         if q_lengths is not None:
