@@ -67,6 +67,26 @@ def test_block_sparse_bwd_matches_oracle(L, D, dtype, density):
         assert rel(g, r) <= TOL, (name, rel(g, r))
 
 
+@pytest.mark.parametrize("L,D,dtype,density", [(1000, 64, torch.bfloat16, 0.25), (1000, 128, torch.bfloat16, 0.25),
+                                               (517, 64, torch.float16, 0.3), (700, 128, torch.float16, 0.4),
+                                               (300, 64, torch.bfloat16, 0.5), (260, 128, torch.bfloat16, 0.6)])
+def test_default_backward_kernels_at_the_rounding_floor(L, D, dtype, density):
+    """The default kernels (hand-placed dK/dV stream, 2-slot dQ) against the fp64 oracle at a bound
+    near their storage-rounding floor instead of TOL: measured 2.3-2.4e-3 (bf16) and 2.9-3.0e-4
+    (f16) relative per gradient (tools/diag/bwd_parity_err.py, gpurun_out r05_c27), bound ~1.7x."""
+    B, H = 1, 2
+    q, k, v, do = (_rand(B, H, L, D, dtype=dtype, seed=s) for s in range(4))
+    nb = (L + 127) // 128
+    mask = O.block_mask_from_density(B, H, nb, nb, density, seed=7)
+    ops = _ops()
+    out, lse = ops.attention_fwd(q.to(DEV), k.to(DEV), v.to(DEV), block_mask=mask.to(DEV), need_lse=True)
+    dq, dk, dv = ops.attention_bwd(do.to(DEV), q.to(DEV), k.to(DEV), v.to(DEV), out, lse, block_mask=mask.to(DEV))
+    rq, rk, rv = O.block_sparse_attention_bwd(q, k, v, out.cpu(), lse.cpu(), do, mask)
+    tight = 4e-3 if dtype == torch.bfloat16 else 6e-4
+    for name, g, r in (("dq", dq, rq), ("dk", dk, rk), ("dv", dv, rv)):
+        assert rel(g, r) <= tight, (name, rel(g, r))
+
+
 @pytest.mark.parametrize("D", [64, 128])
 def test_pipeline_dkdv_agrees_with_round3_kernel(D, monkeypatch):
     """The hand-scheduled dK/dV kernels (vb_attn_bwd_kv.hip, default) against the round-3
@@ -197,27 +217,30 @@ def _realistic(B, H, L, D, seed):
     return q, k, v, do
 
 
-def _check_adaptive_grads(m, cfg, q, k, v, do):
+def _check_adaptive_grads(m, cfg, q, k, v, do, tight=None):
+    tight = tight or {}
     qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
     out = m(qd, kd, vd)
     out.backward(do.to(DEV))
     mask = m.last_mask.bool().cpu()
     fwd = O.adaptive_attention(q, k, v, cfg, None, None, mask=mask)
-    assert rel(out.detach().float().cpu(), fwd["out"]) <= TOL
+    assert rel(out.detach().float().cpu(), fwd["out"]) <= tight.get("out", TOL)
     rq, rk, rv = O.adaptive_attention_bwd(q, k, v, do, cfg, fwd)
     for name, g, r in (("dq", qd.grad, rq), ("dk", kd.grad, rk), ("dv", vd.grad, rv)):
         assert torch.isfinite(g).all(), name
-        assert rel(g, r) <= TOL, (name, rel(g, r))
+        assert rel(g, r) <= tight.get(name, TOL), (name, rel(g, r))
 
 
 @pytest.mark.parametrize("variant,H,D", [("cog", 2, 64), ("wan", 2, 128)])
 def test_adaptive_module_backward_matches_oracle(variant, H, D):
     """Training path (grad enabled): the reference's two-branch autograd — alpha detached,
-    pooled-branch K/V grads through the mean pool, Gilbert gather transposed."""
+    pooled-branch K/V grads through the mean pool, Gilbert gather transposed. Besides TOL, a bound
+    near the measured errors (r05_c27: out 2.0e-3 / 1.7e-3, dq 8.0e-3 / 7.9e-3 — the bf16 combine
+    weight and both branches' dS — dk 3.1e-3 / 2.5e-3, dv 2.5e-3 / 2.3e-3)."""
     m, cfg = _small_module(variant)
     L = m.gilbert_rearranger.seq_len
     q, k, v, do = _realistic(1, H, L, D, seed=3)
-    _check_adaptive_grads(m, cfg, q, k, v, do)
+    _check_adaptive_grads(m, cfg, q, k, v, do, tight=dict(out=3e-3, dq=1.2e-2, dk=5e-3, dv=4e-3))
 
 
 @pytest.mark.parametrize("variant,D", [("cog", 64), ("wan", 128)])
