@@ -554,3 +554,39 @@ def test_reference_signature_varlen_with_an_empty_sequence():
         got = out[s0:s0 + n].transpose(0, 1)[None].float().cpu()
         assert (got - ref).abs().max() <= 2.5e-2
         assert (lse[b, :, :n].cpu() - ref_lse[0]).abs().max() <= 2e-3
+
+
+@pytest.mark.parametrize("B,H,L,D,heavy,window", [(2, 3, 300, 64, 0, 0), (2, 3, 1000, 128, 2, 0),
+                                                  (1, 5, 777, 64, 2, 3), (3, 2, 520, 64, 9, 1000),
+                                                  (1, 1, 100, 128, 0, 0)])
+def test_dispatch_order_small_shapes_batches_and_windows(B, H, L, D, heavy, window):
+    """The ordered launch at small, ragged, batched shapes: heavy rows beyond nbq, windows larger
+    than an XCD range, ranges with one or no item. Same output as the kernel's own order (bit for
+    bit) and a valid permutation of every range (head-major, longest first within a head)."""
+    from vblade import ops
+    q, k, v = (_rand(B, H, L, D, seed=s).to(DEV) for s in (80, 81, 82))
+    nb = (L + 127) // 128
+    mask = O.block_mask_from_density(B, H, nb, nb, 0.5, seed=83).to(DEV)
+    kept = (mask != 0).sum(-1).to(torch.int32).contiguous()
+    ref = ops.attention_fwd(q, k, v, block_mask=mask, heavy_rows=heavy)
+    qo = torch.full((B * H * nb,), -1, dtype=torch.int32, device=DEV)
+    got = ops.attention_fwd(q, k, v, block_mask=mask, heavy_rows=heavy, order=True, q_lengths=kept,
+                            order_window=window, q_order_out=qo)
+    got2 = ops.attention_fwd(q, k, v, block_mask=mask, heavy_rows=heavy, order=True, order_window=window)
+    assert torch.equal(got, ref) and torch.equal(got2, ref)
+    qo, kc = qo.cpu(), kept.view(-1).cpu()
+    rows_left = nb - min(heavy, nb)
+    nwg = rows_left * B * H
+    q8, r8 = nwg // 8, nwg % 8
+    for x in range(8):
+        start = x * (q8 + 1) if x < r8 else r8 * (q8 + 1) + (x - r8) * q8
+        count = q8 + (1 if x < r8 else 0)
+        if count <= 0:
+            continue
+        skip = count - window if 0 < window < count else 0
+        seg = qo[start:start + count].tolist()
+        assert sorted(seg) == list(range(start, start + count)), (x, seg)
+        assert seg[:skip] == list(range(start, start + skip))
+        keys = [(lin // rows_left, -int(kc[(lin // rows_left) * nb + rows_left - 1 - lin % rows_left]))
+                for lin in seg[skip:]]
+        assert keys == sorted(keys), (x, keys)
