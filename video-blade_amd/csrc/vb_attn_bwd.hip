@@ -128,12 +128,23 @@ __global__ void __launch_bounds__(256) bwd_prep_kernel(const PrepParams p) {
 #ifndef VB_DKDV_WAVES_D64
 #define VB_DKDV_WAVES_D64 2   // waves per SIMD the D=64 dK/dV kernel is register-budgeted for
 #endif
+#ifndef VB_ML_PYR_WAVES
+// waves per multi-level pooled dK/dV workgroup at D=64: 2 = 64-row items on a 2-slot ring, four
+// workgroups per CU (vb_ml_attn_bwd 1.15x over 4 = 128-row items, dk bit-identical;
+// profiles/r05_ml_bwd_pyr2_ab.log). D=128 keeps 4 (two waves spill there).
+#define VB_ML_PYR_WAVES 2
+#endif
 #ifndef VB_ML_LONG_FIRST
 #define VB_ML_LONG_FIRST 1   // multi-level pooled dK/dV items in level 8, 4, 2 order (longest first; 0: 2, 4, 8)
 #endif
-template <int D, class T, bool kPooled, bool kML = false>
-__global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D64) bwd_dkdv_kernel(const BwdParams p) {
+// kW: waves per workgroup (4, or 2 for the multi-level pooled items: an item is 32 kW pyramid rows,
+// so a level-2 item covers one key block and walks its own q-list instead of a union, and a level-4
+// or level-8 item half as many blocks; the union walk leaves fewer waves idle).
+template <int D, class T, bool kPooled, bool kML = false, int kW = 4>
+__global__ void __launch_bounds__(kW * 64, D == 128 ? 1 : VB_DKDV_WAVES_D64) bwd_dkdv_kernel(const BwdParams p) {
   using namespace bwd;
+  static_assert(kW == 4 || (kML && kPooled), "2-wave workgroups: the multi-level pooled items only");
+  constexpr int kRows = 32 * kW;             // keys (pyramid rows) per work item
   // s_setprio 1 around the MFMA chains (bit 0: S and dP, bit 1: the dV/dK steps)
   constexpr int kPrioKV = D == 128 ? VB_DKDV_PRIO128 : VB_DKDV_PRIO64;
   constexpr int KS = D / 16;
@@ -145,7 +156,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   constexpr int kCh = RB / 16;
   constexpr int kInst = 2 * kInstTile + 1;  // Q, dO, stats (1 KiB)
   constexpr int kBufBytes = 2 * kTileBytes + 1024;
-  constexpr int kBufs = 3;                   // LDS ring: tile t read, t+1 in flight, t+2 being issued
+  // LDS ring: tile t read, t+1 in flight, t+2 being issued; kW = 2: a 2-slot ring (38 KiB with the
+  // lists), so four 2-wave workgroups fit a CU (two waves per SIMD, as the 4-wave form)
+  constexpr int kBufs = kW == 2 ? 2 : 3;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kBufs * kBufBytes + kMaxBlocks * 3 + 16];
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
   int* list_n = reinterpret_cast<int*>(smem + kBufs * kBufBytes + kMaxBlocks * 2);
@@ -172,10 +185,10 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
     // longest items first: a level-8 block's q-list is the union over 8 key blocks (≈4x a level-2
     // item's tiles), so level 8, then 4, then 2, each spread over the heads (consecutive
     // workgroups = different heads, so different XCDs); placement only, the results are the same
-    const MlGeom gm(p.Lpad);
     int lin = (int)blockIdx.x;
     ml_e = 3;
-    while (ml_e > 1 && lin >= gm.nblk[ml_e] * BH) { lin -= gm.nblk[ml_e] * BH; --ml_e; }
+    auto nit = [&](int e) { return ((p.Lpad >> e) + kRows - 1) / kRows; };   // items of level e
+    while (ml_e > 1 && lin >= nit(ml_e) * BH) { lin -= nit(ml_e) * BH; --ml_e; }
     bh = lin % BH;
     ml_m = lin / BH;
     kblk = 0;
@@ -214,11 +227,12 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
     const MlGeom gm(p.Lpad);
     if (kPooled && !VB_ML_LONG_FIRST) {
       ml_e = 1;
-      while (ml_e < 3 && ml_m >= gm.nblk[ml_e]) { ml_m -= gm.nblk[ml_e]; ++ml_e; }
+      auto nit = [&](int e) { return ((p.Lpad >> e) + kRows - 1) / kRows; };
+      while (ml_e < 3 && ml_m >= nit(ml_e)) { ml_m -= nit(ml_e); ++ml_e; }
     }
     ml_row0 = gm.off[ml_e];
     Lkey = kPooled ? p.Lpad >> ml_e : Lk;
-    k0 = ml_m * kBlk;
+    k0 = ml_m * (kPooled ? kRows : kBlk);
   }
   if (k0 >= Lkey || Lq <= 0) return;
   const int nbq = (Lq + kBlk - 1) / kBlk;
@@ -227,7 +241,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   const uint8_t* mcol = nullptr;
   if (!kPooled || kML) {
     const uint8_t* mh = head_mask_base(p.mask, p.ms, p.head_mask_type, p.H, b, h, nan_head, p.hm_mode);
-    if (mh) mcol = mh + (kML ? (ml_m << ml_e) : kblk);
+    if (mh) mcol = mh + (kML ? ((k0 << ml_e) >> 7) : kblk);   // the item's first key block
   }
   const int qlo = (kPooled && !kML) ? split * nbq / p.psplit : 0;
   const int qhi = (kPooled && !kML) ? (split + 1) * nbq / p.psplit : nbq;
@@ -235,7 +249,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
     // q-blocks where any of this item's 2^e key blocks has level 2^e; bit e' = block ml_m*2^e + e'
     if (threadIdx.x < 64) {
       const int pl = 1 << ml_e;
-      const int nblk_here = min(pl, p.nbk - (ml_m << ml_e));
+      const int nblk_here = min((kRows << ml_e) >> 7, p.nbk - ((k0 << ml_e) >> 7));
       int n = 0;
       for (int i0 = 0; i0 < nbq; i0 += 64) {
         const int i = i0 + lane;
@@ -307,15 +321,15 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   // issues instructions i = wave + 4k (i < kInstTile: Q, then dO, then the stats KiB). A lane's
   // part of each instruction (row within the tile, swizzled chunk) is a fixed voffset; the tile's
   // first row is the scalar soffset. Rows past Lq read as zeros (their stats make P = 0).
-  constexpr int kHi = (kInst + 3) / 4, kLo = kInst / 4;  // DMA instructions per wave and tile
-  const bool many = wave < (kInst & 3);
+  constexpr int kHi = (kInst + kW - 1) / kW, kLo = kInst / kW;  // DMA instructions per wave and tile
+  const bool many = wave < (kInst % kW);
   const srd_t q_srd = make_srd(qsrc, (int)((int64_t)(Lq - 1) * qrowb + RB));
   const srd_t do_srd = make_srd(dosrc, (int)((int64_t)(Lq - 1) * dorowb + RB));
   const srd_t st_srd = make_srd(stsrc, p.ntile * 1024);
   int voff[kHi];
 #pragma unroll
   for (int k = 0; k < kHi; ++k) {
-    const int i = wave + 4 * k;
+    const int i = wave + kW * k;
     voff[k] = lane * 16;
     if (i < 2 * kInstTile) {
       const int ii = i < kInstTile ? i : i - kInstTile;
@@ -330,7 +344,7 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
     uint8_t* buf = smem + slot * kBufBytes;
 #pragma unroll
     for (int k = 0; k < kHi; ++k) {
-      const int i = wave + 4 * k;
+      const int i = wave + kW * k;
       if (i >= kInst) break;
       if (i < kInstTile) dma16(q_srd, buf + i * 1024, voff[k], row0 * qrowb);
       else if (i < 2 * kInstTile) dma16(do_srd, buf + i * 1024, voff[k], row0 * dorowb);
@@ -349,20 +363,24 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   constexpr bool kSeed = D == 64 || VB_BWD_SEED128;
 
   if (ntiles > 0) issue(0, 0);
-  if (ntiles > 1) issue(1, 1);
+  if (kBufs == 3 && ntiles > 1) issue(1, 1);
   // The loop body is instantiated once per ring slot: every LDS address is a compile-time offset.
   auto body = [&](int t, auto U) __attribute__((always_inline)) {
     constexpr int u_slot = decltype(U)::value;
     // retire this wave's DMAs of tile t (tile t+1 stays in flight); the barrier makes every wave's
     // part visible and proves slot (t-1) % kBufs is no longer being read
-    if (t + 1 < ntiles) {
+    if (kBufs == 3 && t + 1 < ntiles) {
       if (many) VB_WAIT_VMCNT(kHi);
       else VB_WAIT_VMCNT(kLo);
     } else {
       VB_WAIT_VMCNT(0);
     }
     __builtin_amdgcn_s_barrier();
-    if (t + 2 < ntiles) issue(t + 2, (u_slot + 2) % kBufs);
+    if constexpr (kBufs == 3) {
+      if (t + 2 < ntiles) issue(t + 2, (u_slot + 2) % kBufs);
+    } else {
+      if (t + 1 < ntiles) issue(t + 1, (u_slot + 1) % kBufs);   // into slot (t-1) % 2, free after the barrier
+    }
     const uint8_t* qt = smem + u_slot * kBufBytes;
     const uint8_t* dot = qt + kTileBytes;
     const float* st = reinterpret_cast<const float*>(qt + 2 * kTileBytes);
@@ -455,7 +473,9 @@ __global__ void __launch_bounds__(bwd::kThreads, D == 128 ? 1 : VB_DKDV_WAVES_D6
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
     body(t0, std::integral_constant<int, 0>{});
     if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
-    if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
+    if constexpr (kBufs == 3) {
+      if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
+    }
   }
 
   // ---- epilogue: lane = key, registers = d ---------------------------------------------------------
@@ -1301,7 +1321,12 @@ template <int D, class T>
 static int launch_ml_grads(const PrepParams& pp, const BwdParams& p, hipStream_t s) {
   if (int rc = launch_prep<T>(pp, s)) return rc;
   const int BH = p.B * p.H;
-  hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true, true>), dim3(p.nbkp * BH), dim3(bwd::kThreads), 0, s, p);
+  {
+    constexpr int kW = D == 64 ? VB_ML_PYR_WAVES : 4, kRows = 32 * kW;   // items of kRows pyramid rows
+    int items = 0;
+    for (int e = 1; e < 4; ++e) items += ((p.Lpad >> e) + kRows - 1) / kRows;
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true, true, kW>), dim3(items * BH), dim3(kW * 64), 0, s, p);
+  }
   if (int rc = check_launch("bwd_dkdv_kernel<multi-level pooled>")) return rc;
   if (ml_dkdv_pipe_enabled()) {
     if (int rc = launch_ml_dkdv_pipe(p, D, std::is_same<T, F16>::value, s)) return rc;
