@@ -74,7 +74,10 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 #define VB_FUSED_POOL_LAST 0   // 1: pooling workgroups after the score workgroups (measured 1-4 % slower)
 #endif
 #ifndef VB_FUSED_POOL_WGS
-#define VB_FUSED_POOL_WGS 512   // workgroups of the predictor's launch that run the pooled K/V pass
+// workgroups of the predictor's launch that run the pooled K/V pass (D=128, Wan). Round 5: with the
+// pass pipelined (vb_pool.hpp) 512 measured 0.995x per Wan call against the serial pass, 320 0.999x,
+// 192 0.995x, 128 0.981x (profiles/r05_pool_pipeline_ab.log)
+#define VB_FUSED_POOL_WGS 320
 #endif
 constexpr int kFusedPoolWgs = VB_FUSED_POOL_WGS;
 #ifndef VB_FUSED_POOL_WGS64

@@ -21,33 +21,50 @@ struct PyrTask {
 // Each level is the mean of the previous level's pairs in fp32, rounded to the storage dtype, as
 // torch.mean on a bf16/fp16 view does. Consecutive items take consecutive chunks of a row, so
 // every row read/write is coalesced. Layout per (b,h): [Lpad level-1 | Lpad/2 | Lpad/4 | Lpad/8].
-template <int D, class T>
-__device__ __forceinline__ void kv_pyramid_span(const PyrTask& t, int64_t idx0, int64_t step) {
+// The `rows` entries of a thread's next item are loaded while the current item's K/V rows are in
+// flight (two entry sets, loop unrolled by two), and K and V share them: one memory round trip per
+// item (round 5; each entry had been loaded behind a wait for the previous row's data).
+template <int D, class T, bool kRows>
+__device__ __forceinline__ void kv_pyramid_steps(const PyrTask& t, int64_t idx0, int64_t step) {
   constexpr int kCh = D / 8;   // 16-byte chunks per row
   const int ngroups = t.Lpad / 8;
   const int64_t total = (int64_t)t.B * t.H * ngroups * kCh;
+  if (idx0 >= total) return;
   const int R = 15 * (t.Lpad / 8);
   const int off2 = t.Lpad, off4 = t.Lpad + t.Lpad / 2, off8 = off4 + t.Lpad / 4;
-  for (int64_t tid = idx0; tid < total; tid += step) {
+  auto positions = [&](int64_t tid, int (&pos)[8]) __attribute__((always_inline)) {
+    const int g = (int)((tid / kCh) % ngroups);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) pos[r] = min(g * 8 + r, t.L - 1);
+    if constexpr (kRows) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) pos[r] = t.rows[pos[r]];
+    }
+  };
+  int64_t tid = idx0;
+  auto run = [&](const int (&cur)[8], int (&nxt)[8]) __attribute__((always_inline)) -> bool {
     const int ch = (int)(tid % kCh);
     const int64_t rest = tid / kCh;
     const int g = (int)(rest % ngroups);
     const int bh = (int)(rest / ngroups);
     const int b = bh / t.H, h = bh % t.H;
+    u32x4 xs[2][8];
 #pragma unroll
     for (int mat = 0; mat < 2; ++mat) {
       const uint8_t* src = mat == 0 ? t.k : t.v;
       const int64_t s0 = mat == 0 ? t.ks[0] : t.vs[0], s1 = mat == 0 ? t.ks[1] : t.vs[1];
       const int64_t s2 = mat == 0 ? t.ks[2] : t.vs[2];
-      uint8_t* dst = (mat == 0 ? t.kpyr : t.vpyr) + ((int64_t)bh * R * D + ch * 8) * 2;
       const uint8_t* base = src + (b * s0 + h * s1 + ch * 8) * 2;
-      u32x4 x[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        int row = min(g * 8 + r, t.L - 1);
-        if (t.rows) row = t.rows[row];
-        x[r] = *reinterpret_cast<const u32x4*>(base + (int64_t)row * s2 * 2);
-      }
+      for (int r = 0; r < 8; ++r) xs[mat][r] = *reinterpret_cast<const u32x4*>(base + (int64_t)cur[r] * s2 * 2);
+    }
+    const int64_t ntid = tid + step;
+    const bool more = ntid < total;
+    positions(more ? ntid : tid, nxt);   // past the last item: reloaded, unused
+#pragma unroll
+    for (int mat = 0; mat < 2; ++mat) {
+      const u32x4* x = xs[mat];
+      uint8_t* dst = (mat == 0 ? t.kpyr : t.vpyr) + ((int64_t)bh * R * D + ch * 8) * 2;
       uint8_t* dst1 = dst + (int64_t)(g * 8) * D * 2;
       uint8_t* dst2 = dst + (int64_t)(off2 + g * 4) * D * 2;
       uint8_t* dst4 = dst + (int64_t)(off4 + g * 2) * D * 2;
@@ -93,7 +110,21 @@ __device__ __forceinline__ void kv_pyramid_span(const PyrTask& t, int64_t idx0, 
         *reinterpret_cast<u32x4*>(dst8) = w;
       }
     }
+    tid = ntid;
+    return more;
+  };
+  int pa[8], pb[8];
+  positions(tid, pa);
+  for (;;) {
+    if (!run(pa, pb)) break;
+    if (!run(pb, pa)) break;
   }
+}
+
+template <int D, class T>
+__device__ __forceinline__ void kv_pyramid_span(const PyrTask& t, int64_t idx0, int64_t step) {
+  if (t.rows) kv_pyramid_steps<D, T, true>(t, idx0, step);
+  else kv_pyramid_steps<D, T, false>(t, idx0, step);
 }
 
 }  // namespace vb
