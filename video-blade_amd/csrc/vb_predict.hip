@@ -71,8 +71,13 @@ template <int D> constexpr int kPBufs = D == 64 ? VB_PRED_BUFS64 : VB_PRED_BUFS;
 #endif
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 #ifndef VB_FUSED_POOL_LAST
-#define VB_FUSED_POOL_LAST 0   // 1: pooling workgroups after the score workgroups (measured 1-4 % slower)
+// pooling workgroups after the score workgroups: D=128 (Wan) only. Round 5, with the pipelined pass:
+// Wan call 1.004-1.006x (launch span 246 -> 232 us), CogVideoX 0.945x (its pass outlasts the score
+// kernel's last round); before the pipelining it measured 1-4 % slower on both
+// (profiles/r05_pool_pipeline_ab.log)
+#define VB_FUSED_POOL_LAST 2   // 0: never, 1: both head dims, 2: D=128 only
 #endif
+template <int D> constexpr bool kPoolLast = VB_FUSED_POOL_LAST == 1 || (VB_FUSED_POOL_LAST == 2 && D == 128);
 #ifndef VB_FUSED_POOL_WGS
 // workgroups of the predictor's launch that run the pooled K/V pass (D=128, Wan). Round 5: with the
 // pass pipelined (vb_pool.hpp) 512 measured 0.995x per Wan call against the serial pass, 320 0.999x,
@@ -466,26 +471,20 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
   // The first n_pool workgroups of the launch run the pooled K/V pass (HBM-bound) beside the score
   // workgroups (MFMA-bound): one launch, no second stream or events. n_pool is a multiple of 8, so
   // the score workgroups keep their XCD (blockIdx % 8).
-#if VB_FUSED_POOL_LAST
-  // pooling workgroups after the score workgroups: they fill the score kernel's last, partial round
-  const int n_score = (int)gridDim.x - p.n_pool;
-  if ((int)blockIdx.x >= n_score) {
-    pool_kv_span<T>(p.pool, (int64_t)((int)blockIdx.x - n_score) * blockDim.x + threadIdx.x, (int64_t)p.n_pool * blockDim.x);
-    return;
-  }
-  const int wg = (int)blockIdx.x;
-#else
-  if ((int)blockIdx.x < p.n_pool) {
+  // kPoolLast<D>: the pooling workgroups come after the score workgroups instead, where they fill the
+  // score kernel's partial last round.
+  const bool pool_wg = kPoolLast<D> ? (int)blockIdx.x >= (int)gridDim.x - p.n_pool : (int)blockIdx.x < p.n_pool;
+  if (pool_wg) {
     VB_TRACE_START(1);
-    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)p.n_pool * blockDim.x;
+    const int pw = kPoolLast<D> ? (int)blockIdx.x - ((int)gridDim.x - p.n_pool) : (int)blockIdx.x;
+    const int64_t i0 = (int64_t)pw * blockDim.x + threadIdx.x, st = (int64_t)p.n_pool * blockDim.x;
     if (p.pool_kind == 2) kv_pyramid_span<D, T>(p.pyr, i0, st);
     else pool_kv_span<T>(p.pool, i0, st);
     VB_TRACE_END();
     return;
   }
   VB_TRACE_START(0);
-  const int wg = (int)blockIdx.x - p.n_pool;
-#endif
+  const int wg = kPoolLast<D> ? (int)blockIdx.x : (int)blockIdx.x - p.n_pool;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nb = p.nb;
   float* mrow_s = reinterpret_cast<float*>(smem);
