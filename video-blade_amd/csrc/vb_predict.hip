@@ -121,7 +121,7 @@ struct PredParams {
   uint8_t* mask;
   unsigned long long* count;
   int32_t* rows_kept;   // [B,H,nb] kept blocks per mask row (nullable)
-  int dbg;   // diagnostic builds only (VB_DEBUG_PRED): 1 = skip epilogue, 2 = skip main loop, 4 = no MFMA
+  int dbg;   // diagnostic builds only (VB_DEBUG_PRED): 1 = skip epilogue, 2 = skip main loop, 4 = no MFMA, 8 = no energy rule
 };
 
 #ifndef VB_DIAG
@@ -838,6 +838,7 @@ __global__ void __launch_bounds__(kPThreads, VB_PRED_MIN_WG) VB_PRED_OCC mask_pr
     }
 #endif
     if (!kEnergy || p.mask == nullptr) return;   // scores only (energy rule elsewhere / not wanted)
+    if (VB_DIAG && (p.dbg & 8)) return;   // diagnostic: no energy rule (Po written)
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     uint8_t* mrow = p.mask + ((int64_t)bh * nb + qb) * nb;
