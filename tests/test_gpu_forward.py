@@ -301,6 +301,29 @@ def test_pool_kv_matches_oracle(L, gap, D):
         assert (got == ref).float().mean() >= 0.99
 
 
+@pytest.mark.parametrize("B,H,L,gap,with_rows", [(1, 3, 1237, 1, True), (1, 3, 1237, 7, False), (1, 3, 1237, 8, True),
+                                                (1, 3, 1237, 9, False), (1, 3, 1237, 16, True), (1, 3, 1237, 30, False),
+                                                (2, 24, 17776, 1, True), (2, 24, 17776, 15, False)])
+def test_pool_kv_pipeline_steps_and_copies(B, H, L, gap, with_rows):
+    """The pooled pass's pipelined steps (vb_pool.hpp: groups of 8 rows, the next step's rows entries
+    loaded one step ahead, two entry sets): gaps below, at and above the group size, with and without
+    the row table; the two large shapes give every thread several items (the launch is capped at
+    kPoolWgsDefault workgroups), so steps chain across items. The Gilbert-order copies are exact."""
+    D = 64
+    k, v = _rand(B, H, L, D, seed=72), _rand(B, H, L, D, seed=73)
+    perm = torch.randperm(L, generator=torch.Generator().manual_seed(2))
+    rows = perm.int().to(DEV) if with_rows else None
+    kp, vp, k_r, v_r = _ops().pool_kv(k.to(DEV), v.to(DEV), gap, rows=rows, reordered=True)
+    src_k, src_v = (k[:, :, perm], v[:, :, perm]) if with_rows else (k, v)
+    assert torch.equal(k_r.cpu(), src_k) and torch.equal(v_r.cpu(), src_v)
+    for got, x in ((kp, src_k), (vp, src_v)):
+        ref = O.simple_pooling(x, gap).float()
+        got = got.float().cpu()
+        ulp = ref.abs().clamp_min(2 ** -126) * 2 ** -7
+        assert torch.all((got - ref).abs() <= ulp + 1e-30)
+        assert (got == ref).float().mean() >= 0.99
+
+
 def test_lse_combine_matches_reference_rounding():
     B, H, L, D = 2, 3, 333, 64
     o1, o2 = _rand(B, H, L, D, seed=80), _rand(B, H, L, D, seed=81)
