@@ -1,0 +1,15 @@
+# Gathered K/V: one kv_rows-entry DMA per kept block (tile pair), issued kBufs bodies ahead (cur) vs the
+# committed per-tile DMA (gbase) and no entry DMA at all (noidx, timing only). Parity first.
+set -o pipefail
+O=gpurun_out/r05_c48
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_module.py tests/test_gpu_fullsize.py tests/test_gpu_config1.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; tail -n 2 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "Error|assert" $O/pytest.log | head -8; exit $rc; }
+for lib in gbase cur noidx gbase cur; do
+  if [ $lib = cur ]; then L=video-blade_amd/vblade/libvblade_hip.so; else L=video-blade_amd/vblade/variants/lib_$lib.so; fi
+  VBLADE_LIB=$L timeout -k 10 300 python -u tools/diag/gather_cost.py cog > $O/cog_$lib.log 2>&1 || exit $?
+  VBLADE_LIB=$L timeout -k 10 300 python -u tools/diag/gather_cost.py wan > $O/wan_$lib.log 2>&1 || exit $?
+  echo "== $lib"; grep -h "attn\|identical" $O/cog_$lib.log $O/wan_$lib.log
+done
+timeout -k 10 400 python -u tools/ab.py gbase cur --what call --variant both --rounds 25 > $O/ab_call.log 2>&1 || exit $?
+grep -h median $O/ab_call.log
