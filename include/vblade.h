@@ -23,7 +23,13 @@
 extern "C" {
 #endif
 
-#define VB_ABI_VERSION 3   /* 2: mask_head_mode argument of vb_block_sparse_attn_fwd/bwd; 3: vb_attn_args.q_order */
+#define VB_ABI_VERSION 4   /* 2: mask_head_mode argument of vb_block_sparse_attn_fwd/bwd; 3: vb_attn_args.q_order;
+                              4: work_queue (persistent forward), kernel_select/kernels_ran (backward) */
+
+/* Work queue of the persistent forward launches (vb_attn_args / vb_ml_attn_args.work_queue): device
+ * int32[VB_WORK_QUEUE_INTS], ALL ZERO before its first use; every launch leaves it zero again. One
+ * queue serves one launch at a time (launches that may overlap, e.g. on two streams, need one each). */
+#define VB_WORK_QUEUE_INTS 288
 
 enum vb_status {
   VB_OK = 0,
@@ -116,6 +122,10 @@ typedef struct vb_attn_args {
   int order_window;       /* > 0: only the last order_window q-blocks of each XCD range are re-ordered
                              (the tail; the rest keeps the kernel's head-major, Gilbert-neighbour
                              order and its L2 reuse); 0: the whole range */
+  int32_t* work_queue;    /* ABI 4, nullable: persistent dispatch — a resident-sized grid whose workgroups
+                             pull q-blocks from per-XCD queues (in the order above) and, once their own
+                             XCD's queue is empty, from the others'. NULL: one workgroup per q-block.
+                             Never affects results. See VB_WORK_QUEUE_INTS. */
 } vb_attn_args;
 int vb_attn_fwd(const vb_attn_args* args, void* stream);
 
@@ -272,7 +282,23 @@ typedef struct vb_attn_bwd_args {
   float scale;              /* <= 0 -> D^-1/2 */
   int dtype;
   int heavy_rows;           /* scheduling hint as in vb_attn_args */
+  int kernel_select;        /* ABI 4: VB_BWD_SEL_* bits, 0 = the default kernels (same results up to the
+                               fp32 summation order; for A/B tests) */
+  int32_t* kernels_ran;     /* ABI 4, HOST memory, nullable: receives the VB_BWD_RAN_* bits of the
+                               kernels this call launched */
 } vb_attn_bwd_args;
+/* kernel_select bits: the earlier kernels each default replaced */
+#define VB_BWD_SEL_DKDV_ROUND3 1   /* dK/dV (main and pooled keys; multi-level: level 1) on bwd_dkdv_kernel
+                                      instead of the hand-placed stream bwd_dkdv_pipe_kernel */
+#define VB_BWD_SEL_DQ_ROUND3 2     /* dQ on bwd_dq_kernel instead of the pipeline bwd_dq_pipe_kernel */
+#define VB_BWD_SEL_DQ_RING4 4      /* D=128 pipeline dQ on the 4-slot ring (one workgroup per CU) */
+/* kernels_ran bits */
+#define VB_BWD_RAN_DKDV_PIPE 1
+#define VB_BWD_RAN_DKDV_ROUND3 2
+#define VB_BWD_RAN_DQ_PIPE_RING2 4
+#define VB_BWD_RAN_DQ_PIPE_RING4 8
+#define VB_BWD_RAN_DQ_ROUND3 16
+#define VB_BWD_RAN_ML_PYRAMID 32   /* the multi-level pooled-level dK/dV pass */
 uint64_t vb_attn_bwd_workspace_size(const vb_attn_bwd_args* args);
 int vb_attn_bwd(const vb_attn_bwd_args* args, void* stream);
 
@@ -342,6 +368,7 @@ typedef struct vb_ml_attn_args {
   int ref_tail;
   int dtype;
   int heavy_rows;              /* last q-block rows known to be dense (the forced rows): dispatched first */
+  int32_t* work_queue;         /* ABI 4, nullable: persistent dispatch as vb_attn_args.work_queue */
 } vb_ml_attn_args;
 int vb_ml_attn_fwd(const vb_ml_attn_args* args, void* stream);
 
@@ -370,6 +397,8 @@ typedef struct vb_ml_attn_bwd_args {
   int ref_tail;
   int dtype;
   int heavy_rows;
+  int kernel_select;           /* ABI 4: as vb_attn_bwd_args (DKDV_ROUND3: the level-1 pass) */
+  int32_t* kernels_ran;        /* ABI 4, HOST memory, nullable: as vb_attn_bwd_args */
 } vb_ml_attn_bwd_args;
 uint64_t vb_ml_attn_bwd_workspace_size(const vb_ml_attn_bwd_args* args);
 int vb_ml_attn_bwd(const vb_ml_attn_bwd_args* args, void* stream);

@@ -38,7 +38,8 @@ def test_every_declared_symbol_is_exported_and_bound(lib):
 
 
 def test_abi_version(lib):
-    assert lib.vb_abi_version() == 3
+    from vblade import _lib
+    assert lib.vb_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_struct_layouts_match_header():
@@ -105,8 +106,14 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     b.D = 96
     assert lib.vb_attn_bwd(ctypes.byref(b), None) == _lib.VB_ERR_UNSUPPORTED
     assert b"head_dim" in lib.vb_last_error()
-    # workspace sizing is pure host arithmetic
+    # kernel_select: unknown bits refused before any launch (ABI 4)
     b.D = 64
+    b.q = b.k = b.v = b.out = b.lse = b.dout = b.dq = b.dk = b.dv = 1 << 20
+    b.kernel_select = 8
+    assert lib.vb_attn_bwd(ctypes.byref(b), None) == _lib.VB_ERR_INVALID
+    assert b"kernel_select" in lib.vb_last_error()
+    b.kernel_select = 0
+    # workspace sizing is pure host arithmetic
     assert lib.vb_attn_bwd_workspace_size(ctypes.byref(b)) >= 2 * 64 * 4 * 4
     assert lib.vb_block_sparse_attn_bwd_workspace_size(1, 1, 128) > 0
     rc = lib.vb_block_sparse_attn_bwd(*([None] * 11), 1, 1, 64, 128, 128, 0.1, 0.0, 0, 0, 1, 0,
@@ -130,6 +137,10 @@ def test_invalid_arguments_return_codes_without_gpu(lib):
     mb.B = mb.H = 1
     mb.L, mb.D = 300, 64
     assert lib.vb_ml_attn_bwd_workspace_size(ctypes.byref(mb)) > 7 * 384 // 8 * 64 * 4 * 2
+    mb.q = mb.kpyr = mb.vpyr = mb.level_mask = mb.out = mb.lse = mb.dout = mb.dq = mb.dk = mb.dv = 1 << 20
+    mb.kernel_select = _lib.VB_BWD_SEL_DQ_RING4     # the multi-level dQ has one ring
+    assert lib.vb_ml_attn_bwd(ctypes.byref(mb), None) == _lib.VB_ERR_INVALID
+    assert b"kernel_select" in lib.vb_last_error()
     assert lib.vb_kv_pyramid(None, None, None, None, None, 1, 1, 1, 64, 0, None, None, None) == _lib.VB_ERR_INVALID
     vals = np.array([3], dtype=np.int32)
     se = np.array([0.0, 1.0], dtype=np.float64)
@@ -180,6 +191,17 @@ def test_mask_predict_option_checks_without_gpu(lib):
     p.mask, p.mask_level = None, 1
     assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
     assert b"mask output" in lib.vb_last_error()
+    # the kept counts come from the energy rule only: refused with the level mask or scores only
+    for level, mask in ((1, 1 << 20), (0, None)):
+        p = args()
+        p.mask_rows_kept = 1 << 20
+        p.mask = mask
+        if level:
+            p.mask_level, p.level_bands = 1, 1
+            p.level_band_value, p.level_band_start, p.level_band_end = (
+                np.array([1], dtype=np.int32).ctypes.data, se[:1].ctypes.data, se[1:].ctypes.data)
+        assert lib.vb_mask_predict(ctypes.byref(p), None) == _lib.VB_ERR_INVALID
+        assert b"mask_rows_kept" in lib.vb_last_error()
 
 
 def test_level_bands_follow_mask_ratio_dict_order():

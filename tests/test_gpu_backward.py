@@ -87,51 +87,92 @@ def test_default_backward_kernels_at_the_rounding_floor(L, D, dtype, density):
         assert rel(g, r) <= tight, (name, rel(g, r))
 
 
+def _lib_bits():
+    from vblade import _lib
+    return _lib
+
+
 @pytest.mark.parametrize("D", [64, 128])
-def test_pipeline_dkdv_agrees_with_round3_kernel(D, monkeypatch):
+def test_default_backward_reports_the_pipeline_kernels(D):
+    """kernel_select = 0 launches the hand-placed dK/dV stream and the 2-slot pipeline dQ, and the
+    call says so (vb_attn_bwd_args.kernels_ran): the tests below compare kernels that really ran."""
+    L = 300
+    q, k, v, do = (_rand(1, 2, L, D, seed=40 + s) for s in range(4))
+    mask = O.block_mask_from_density(1, 2, 3, 3, 0.6, seed=1)
+    ops, lib = _ops(), _lib_bits()
+    qd, kd, vd, dod, md = (t.to(DEV) for t in (q, k, v, do, mask))
+    out, lse = ops.attention_fwd(qd, kd, vd, block_mask=md, need_lse=True)
+    ran = []
+    ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md, kernels_ran=ran)
+    assert ran == [lib.VB_BWD_RAN_DKDV_PIPE | lib.VB_BWD_RAN_DQ_PIPE_RING2]
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_pipeline_dkdv_agrees_with_round3_kernel(D):
     """The hand-scheduled dK/dV kernels (vb_attn_bwd_kv.hip, default) against the round-3
-    bwd_dkdv_kernel (VB_BWD_KV64/128=0) on the same inputs: bit-identical at D=64 (the same -Delta
-    seeding and summation order), within bf16 rounding at D=128 (the pipeline seeds dP with -Delta,
-    the round-3 D=128 kernel added it after the chain). dQ is the same kernel in both runs."""
+    bwd_dkdv_kernel (kernel_select VB_BWD_SEL_DKDV_ROUND3) on the same inputs, each launch's kernels
+    asserted from kernels_ran: bit-identical at D=64 (the same -Delta seeding and summation order),
+    within bf16 rounding at D=128 (the pipeline seeds dP with -Delta, the round-3 D=128 kernel added it
+    after the chain). dQ is the same kernel in both runs. Both against the fp64 oracle too."""
     B, H, L = 1, 2, 700
     q, k, v, do = (_rand(B, H, L, D, seed=20 + s) for s in range(4))
     nb = (L + 127) // 128
     mask = O.block_mask_from_density(B, H, nb, nb, 0.5, seed=3)
-    ops = _ops()
+    ops, lib = _ops(), _lib_bits()
     qd, kd, vd, dod, md = (t.to(DEV) for t in (q, k, v, do, mask))
     out, lse = ops.attention_fwd(qd, kd, vd, block_mask=md, need_lse=True)
-    env = "VB_BWD_KV64" if D == 64 else "VB_BWD_KV128"
-    monkeypatch.setenv(env, "1")
-    new = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
-    monkeypatch.setenv(env, "0")
-    old = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
+    ran_new, ran_old = [], []
+    new = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md, kernels_ran=ran_new)
+    old = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md,
+                            kernel_select=lib.VB_BWD_SEL_DKDV_ROUND3, kernels_ran=ran_old)
+    assert ran_new == [lib.VB_BWD_RAN_DKDV_PIPE | lib.VB_BWD_RAN_DQ_PIPE_RING2]
+    assert ran_old == [lib.VB_BWD_RAN_DKDV_ROUND3 | lib.VB_BWD_RAN_DQ_PIPE_RING2]
     assert torch.equal(new[0], old[0])                      # dq
     for a, b in zip(new[1:], old[1:]):
         if D == 64:
             assert torch.equal(a, b)
         else:
             assert rel(a.float().cpu(), b.float().cpu()) <= 5e-3
+    rq, rk, rv = O.block_sparse_attention_bwd(q, k, v, out.cpu(), lse.cpu(), do, mask)
+    for g, r in zip(old, (rq, rk, rv)):
+        assert rel(g, r) <= 4e-3
 
 
-@pytest.mark.parametrize("D", [64, 128])
-def test_pipeline_dq_agrees_with_round3_kernel(D, monkeypatch):
-    """The hand-scheduled dQ (default at D=64, opt-in VB_BWD_DQ128=1 at D=128) stays correct:
-    against the round-3 dQ kernel (VB_BWD_DQ64/128=0) on a ragged length with a partial last key tile."""
+@pytest.mark.parametrize("D,sel", [(64, "round3"), (128, "round3"), (64, "ring4"), (128, "ring4")])
+def test_pipeline_dq_agrees_with_selected_kernels(D, sel):
+    """The default dQ (2-slot pipeline) against the round-3 bwd_dq_kernel (VB_BWD_SEL_DQ_ROUND3) and
+    the 4-slot pipeline (VB_BWD_SEL_DQ_RING4) on a ragged length with a partial last key tile: each
+    launch's kernels asserted from kernels_ran, dk/dv identical (the same dK/dV kernel), dq within
+    bf16 rounding of the default and at the oracle's rounding floor."""
     B, H, L = 1, 2, 517
     q, k, v, do = (_rand(B, H, L, D, seed=30 + s) for s in range(4))
     nb = (L + 127) // 128
     mask = O.block_mask_from_density(B, H, nb, nb, 0.5, seed=4)
-    ops = _ops()
+    ops, lib = _ops(), _lib_bits()
     qd, kd, vd, dod, md = (t.to(DEV) for t in (q, k, v, do, mask))
     out, lse = ops.attention_fwd(qd, kd, vd, block_mask=md, need_lse=True)
-    env = "VB_BWD_DQ64" if D == 64 else "VB_BWD_DQ128"
-    monkeypatch.setenv(env, "1")
-    new = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
-    monkeypatch.setenv(env, "0")
-    old = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md)
-    assert torch.isfinite(new[0]).all()
+    bit = lib.VB_BWD_SEL_DQ_ROUND3 if sel == "round3" else lib.VB_BWD_SEL_DQ_RING4
+    ran_bit = lib.VB_BWD_RAN_DQ_ROUND3 if sel == "round3" else lib.VB_BWD_RAN_DQ_PIPE_RING4
+    ran_new, ran_old = [], []
+    new = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md, kernels_ran=ran_new)
+    old = ops.attention_bwd(dod, qd, kd, vd, out, lse, block_mask=md, kernel_select=bit, kernels_ran=ran_old)
+    assert ran_new == [lib.VB_BWD_RAN_DKDV_PIPE | lib.VB_BWD_RAN_DQ_PIPE_RING2]
+    assert ran_old == [lib.VB_BWD_RAN_DKDV_PIPE | ran_bit]
+    assert torch.isfinite(old[0]).all()
     assert rel(new[0].float().cpu(), old[0].float().cpu()) <= 5e-3
     assert torch.equal(new[1], old[1]) and torch.equal(new[2], old[2])
+    rq, _, _ = O.block_sparse_attention_bwd(q, k, v, out.cpu(), lse.cpu(), do, mask)
+    assert rel(old[0], rq) <= 4e-3
+
+
+def test_kernel_select_rejects_unknown_bits():
+    L, D = 128, 64
+    q, k, v, do = (_rand(1, 1, L, D, seed=s).to(DEV) for s in range(4))
+    ops = _ops()
+    from vblade import _lib
+    out, lse = ops.attention_fwd(q, k, v, need_lse=True)
+    with pytest.raises(_lib.VBladeError):
+        ops.attention_bwd(do, q, k, v, out, lse, kernel_select=8)
 
 
 def test_bwd_empty_rows_and_columns_and_determinism():

@@ -413,6 +413,84 @@ def test_longest_first_dispatch_order_is_bit_identical(variant, H, D):
                 assert keys == sorted(keys), (x, "not longest first within each head")
 
 
+@pytest.mark.parametrize("variant,H,D", [("cog", 8, 64), ("wan", 4, 128)])
+def test_persistent_dispatch_is_bit_identical(variant, H, D):
+    """Round 6 scheduling: with ``persistent`` the attention launch is resident-sized and its
+    workgroups pull q-blocks from per-XCD queues (vb_attn_args.work_queue), then from the other
+    XCDs' queues. Every launch form (module, op with and without the longest-first order, gathered
+    K/V, the LSE-returning training launch) gives the one-workgroup-per-q-block bits, the queue is
+    zero again after every launch, and two streams with their own queues run concurrently."""
+    import vblade
+    from vblade import ops
+    m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+    L = m.gilbert_rearranger.seq_len
+    g = torch.Generator(device=DEV).manual_seed(11)
+    q, k, v = (torch.randn(1, H, L, D, generator=g, device=DEV).to(torch.bfloat16) for _ in range(3))
+    offs = torch.zeros(1, H, 32, dtype=torch.int32, device=DEV) + torch.arange(32, dtype=torch.int32, device=DEV)
+    with torch.no_grad():
+        m.persistent = False
+        ref = m(q, k, v, q_off=offs, k_off=offs)
+        m.persistent = True
+        for _ in range(3):
+            assert torch.equal(m(q, k, v, q_off=offs, k_off=offs), ref)
+        rows = m._rows(q.device)
+        _, mask = m.predict_mask(q, k, offs, offs)
+        kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
+        kw = dict(block_mask=mask, q_rows=rows, kp=kp, vp=vp, kp_log_bias=m._log_gap(q.dtype),
+                  heavy_rows=m.force_tail)
+        a = ops.attention_fwd(q, k_r, v_r, **kw)
+        for order in (False, True):
+            assert torch.equal(ops.attention_fwd(q, k_r, v_r, order=order, persistent=True, **kw), a)
+        assert torch.equal(ops.attention_fwd(q, k, v, kv_rows=rows, persistent=True, **kw),
+                           ops.attention_fwd(q, k, v, kv_rows=rows, **kw))
+        o1, l1 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True)
+        o2, l2 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True, persistent=True)
+        assert torch.equal(o1, o2) and torch.equal(l1, l2)
+        assert int(ops.work_queue(q.device).abs().sum()) == 0
+        # two streams, each its own queue, launched back to back so they overlap
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        torch.cuda.synchronize()
+        outs = []
+        for st in (s1, s2):
+            with torch.cuda.stream(st):
+                outs.append(ops.attention_fwd(q, k_r, v_r, persistent=True, **kw))
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, a) for o in outs)
+        for st in (s1, s2):
+            with torch.cuda.stream(st):
+                assert int(ops.work_queue(q.device).abs().sum()) == 0
+
+
+def test_order_launch_sorts_by_length_when_a_range_spans_too_many_heads():
+    """attn_order_kernel bins (head, kept) keys in LDS; an XCD range spanning more heads than the
+    bins hold (here 2752 heads x 3 lengths > 8192) is sorted by kept count alone (longest first over
+    the range). Outputs stay bit-identical and each range is a permutation in that order."""
+    from vblade import ops
+    B, H, L, D = 4, 5504, 256, 64
+    g = torch.Generator(device=DEV).manual_seed(3)
+    q, k, v = (torch.randn(B, H, L, D, generator=g, device=DEV).to(torch.bfloat16) for _ in range(3))
+    mask = (torch.rand(B, H, 2, 2, generator=g, device=DEV) < 0.5)
+    mask[..., 0] = True
+    mask = mask.to(torch.uint8)
+    with torch.no_grad():
+        a = ops.attention_fwd(q, k, v, block_mask=mask)
+        qo = torch.full((B * H * 2,), -1, dtype=torch.int32, device=DEV)
+        b = ops.attention_fwd(q, k, v, block_mask=mask, order=True, q_order_out=qo)
+        assert torch.equal(a, b)
+    kept = (mask != 0).sum(-1).view(-1).cpu()
+    qo = qo.cpu()
+    nwg = B * H * 2
+    q8, r8 = nwg // 8, nwg % 8
+    for x in range(8):
+        start = x * (q8 + 1) if x < r8 else r8 * (q8 + 1) + (x - r8) * q8
+        count = q8 + (1 if x < r8 else 0)
+        seg = qo[start:start + count]
+        assert torch.equal(seg.sort().values, torch.arange(start, start + count, dtype=torch.int32))
+        bh, qb = seg // 2, 1 - seg % 2
+        lens = kept[bh * 2 + qb]
+        assert bool((lens[:-1] >= lens[1:]).all()), (x, "not longest first")
+
+
 def test_sample_offsets_match_torch_topk_and_rng_order():
     """vb_sample_offsets == torch.topk(rand, 32).indices (the reference's random_sample_tokens,
     :45-46), and the module draws q then k from the same generator stream as the reference."""

@@ -385,3 +385,51 @@ def test_ml_backward_deterministic_and_module_autograd():
         out_inf = mod(q, k, v, level_mask=mask)
     assert (out_inf.float() - out.detach().float()).abs().max().item() <= 2.5e-2
     assert _rel(out_inf.float().cpu(), out.detach().float().cpu()) <= 5e-3
+
+
+@pytest.mark.parametrize("sel", ["default", "dkdv_round3", "dq_round3"])
+def test_ml_backward_kernel_select_matches_oracle(sel):
+    """Every selectable multi-level backward path (kernel_select) against the oracle, with the kernels
+    that ran asserted from kernels_ran: the default (pipeline level-1 dK/dV and dQ), the round-3
+    level-1 dK/dV, the round-3 dQ. dk/dv of the two dK/dV kernels agree to bf16 rounding, dq of the
+    two dQ kernels too; the 4-slot dQ ring does not exist here and is refused."""
+    from vblade import _lib
+    B, H, L, D = 1, 2, 700, 64
+    q, k, v, do = (_rand(B, H, L, D, seed=s) for s in (80, 81, 82, 83))
+    nb = (L + 127) // 128
+    mask = _random_levels(B, H, nb, seed=84, p=(0.15, 0.15, 0.15, 0.25, 0.3))
+    kp, vp = _ops().kv_pyramid(k.to(DEV), v.to(DEV))
+    md = mask.to(torch.uint8).to(DEV)
+    qd, dod = q.to(DEV), do.to(DEV)
+    out, lse = _ops().ml_attention_fwd(qd, kp, vp, md, want_lse=True)
+    bits = {"default": 0, "dkdv_round3": _lib.VB_BWD_SEL_DKDV_ROUND3, "dq_round3": _lib.VB_BWD_SEL_DQ_ROUND3}[sel]
+    want = _lib.VB_BWD_RAN_ML_PYRAMID
+    want |= _lib.VB_BWD_RAN_DKDV_ROUND3 if sel == "dkdv_round3" else _lib.VB_BWD_RAN_DKDV_PIPE
+    want |= _lib.VB_BWD_RAN_DQ_ROUND3 if sel == "dq_round3" else _lib.VB_BWD_RAN_DQ_PIPE_RING2
+    ran, ran0 = [], []
+    g = _ops().ml_attention_bwd(dod, qd, kp, vp, md, out, lse, kernel_select=bits, kernels_ran=ran)
+    g0 = _ops().ml_attention_bwd(dod, qd, kp, vp, md, out, lse, kernels_ran=ran0)
+    assert ran == [want]
+    for a, b in zip(g, g0):
+        assert _rel(a.float().cpu(), b.float().cpu()) <= 5e-3
+    fwd = ML.multilevel_attention(q, k, v, mask)
+    ref = ML.multilevel_attention_bwd(q, k, v, mask, out.float().cpu(), fwd["l"], fwd["m"], do)
+    for name, got, r in zip(("dq", "dk", "dv"), g, ref):
+        assert _rel(got.float().cpu(), r) <= 2e-2, name
+    with pytest.raises(_lib.VBladeError):
+        _ops().ml_attention_bwd(dod, qd, kp, vp, md, out, lse, kernel_select=_lib.VB_BWD_SEL_DQ_RING4)
+
+
+@pytest.mark.parametrize("L,D,H", [(17776, 64, 4), (32760, 128, 2)])
+def test_ml_forward_persistent_is_bit_identical(L, D, H):
+    """The persistent (work-queue) multi-level launch gives the one-workgroup-per-q-block launch's
+    bits, twice in a row on the same queue (which each launch leaves zero)."""
+    q, k, v = (_rand(1, H, L, D, seed=s) for s in (90, 91, 92))
+    nb = (L + 127) // 128
+    mask = _ops().level_mask(_tie_heavy_po(1, H, nb, seed=93).to(DEV))
+    kp, vp = _ops().kv_pyramid(k.to(DEV), v.to(DEV))
+    qd = q.to(DEV)
+    ref = _ops().ml_attention_fwd(qd, kp, vp, mask)
+    for _ in range(2):
+        assert torch.equal(_ops().ml_attention_fwd(qd, kp, vp, mask, persistent=True), ref)
+    assert int(_ops().work_queue(qd.device).abs().sum()) == 0

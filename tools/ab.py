@@ -7,7 +7,9 @@ draws made by torch.rand instead of inside the sampling launch (ops.PHILOX_DRAWS
 with the multi-level mask as its own vb_level_mask launch (--what mlcall: the multi-level module),
 "@noorder" with the attention launches in the kernel's own q-block order (no longest-first sort),
 "@win:N" with only the last N q-blocks of each XCD range re-ordered,
-"@env:VAR=VAL+VAR=VAL" with those environment variables set around its launches. The library latches
+"@env:VAR=VAL+VAR=VAL" with those environment variables set around its launches, "@persist" with the
+persistent (work-queue) attention launch (ops.attention_fwd persistent=True; off otherwise),
+"@sel:N" with the backward's kernel_select bits N (--what bwd / mlbwd). The library latches
 its VB_BWD_* kernel switches once per process (at its first backward call), so A/B a switch with a
 build variant instead (VB_EXTRA_FLAGS=-DVB_BWD_DQ128_DEFAULT=1 tools/build_variant.sh TAG)."""
 import argparse
@@ -42,7 +44,7 @@ def load(tag):
     return lib
 
 
-ORDER = [True, 0]
+ORDER = [True, 0, False, 0]   # longest-first order, order window, persistent launch, backward kernel_select
 
 
 def select(tag, libs):
@@ -50,9 +52,13 @@ def select(tag, libs):
     _lib._lib = libs[tag]
     ORDER[0] = "@noorder" not in tag
     ORDER[1] = 0
+    ORDER[2] = "@persist" in tag
+    ORDER[3] = 0
     for part in tag.split("@")[1:]:
         if part.startswith("win:"):
             ORDER[1] = int(part[4:])
+        if part.startswith("sel:"):
+            ORDER[3] = int(part[4:])
     ops.PHILOX_DRAWS = "@torchrand" not in tag
     multilevel.FUSED_LEVEL_MASK = "@lvsep" not in tag
     for kv in ENV_SET:
@@ -96,10 +102,10 @@ def main():
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, kp=kp,  # noqa
                                            vp=vp, kp_log_bias=m._log_gap(q.dtype),
                                            heavy_rows=m.force_tail, order=ORDER[0], q_lengths=qlen,
-                                           order_window=ORDER[1])
+                                           order_window=ORDER[1], persistent=ORDER[2])
         elif a.what == "fwdlse":   # the training forward's main branch (LSE out: the non-lazy kernel)
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,  # noqa
-                                           heavy_rows=m.force_tail)[0]
+                                           heavy_rows=m.force_tail, persistent=ORDER[2])[0]
             fl = attn_flops(mask, L, D, 0)
         elif a.what == "pred":
             fn = lambda: m.predict_mask(q, k, qo, ko)  # noqa
@@ -113,21 +119,32 @@ def main():
             _, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
             fn = lambda: ops.attention_bwd(do, q, k_r, v_r, out1, lse1, block_mask=mask, q_rows=rows,  # noqa
                                            kv_rows=rows, kp=kp, vp=vp, out2=out2, lse2=lse2,
-                                           alpha=alpha, gap=gap, heavy_rows=m.force_tail)
+                                           alpha=alpha, gap=gap, heavy_rows=m.force_tail,
+                                           kernel_select=ORDER[3])
             fl = 2.5 * fl
         elif a.what == "mlbwd":   # the multi-level path's backward (vb_ml_attn_bwd), dk compared
             do = torch.randn_like(q)
             _, lmask = multilevel.predict_level_mask(q, k, rows=rows)
             kpy, vpy = ops.kv_pyramid(k, v, rows)
             mo, mlse = ops.ml_attention_fwd(q, kpy, vpy, lmask, q_rows=rows, want_lse=True, heavy_rows=2)
-            fn = lambda: ops.ml_attention_bwd(do, q, kpy, vpy, lmask, mo, mlse, rows=rows)[1]  # noqa
+            fn = lambda: ops.ml_attention_bwd(do, q, kpy, vpy, lmask, mo, mlse, rows=rows,  # noqa
+                                              kernel_select=ORDER[3])[1]
             fl = 2.5 * ml_attn_flops(lmask, L, D)
+        elif a.what == "mlattn":   # the multi-level attention launch alone
+            _, lmask = multilevel.predict_level_mask(q, k, rows=rows)
+            kpy, vpy = ops.kv_pyramid(k, v, rows)
+            fn = lambda: ops.ml_attention_fwd(q, kpy, vpy, lmask, q_rows=rows, heavy_rows=2,  # noqa
+                                              persistent=ORDER[2])
+            fl = ml_attn_flops(lmask, L, D)
         elif a.what == "mlcall":   # the multi-level (VBench) module, whole call
             mlm = multilevel.AdaptiveBlockSparseAttnTrain(log_every=0)
-            fn = lambda: mlm(q, k, v)  # noqa
+
+            def fn():
+                mlm.persistent = ORDER[2]
+                return mlm(q, k, v)
         else:
             def fn():
-                m.order, m.order_window = ORDER[0], ORDER[1]
+                m.order, m.order_window, m.persistent = ORDER[0], ORDER[1], ORDER[2]
                 return m(q, k, v)
         ref = None
         times = {kk: [] for kk in keys}
@@ -141,7 +158,7 @@ def main():
                         ref = out[1].clone()
                     else:
                         print(f"  {t}: mask identical to {a.tags[0]}: {torch.equal(out[1], ref)}")
-                if a.what in ("attn", "fwdlse", "bwd", "mlbwd"):
+                if a.what in ("attn", "fwdlse", "bwd", "mlbwd", "mlattn"):
                     outs = tuple(out) if isinstance(out, tuple) else (out,)   # bwd: dq, dk, dv
                     if ref is None:
                         ref = tuple(o.clone() for o in outs)
@@ -165,7 +182,7 @@ def main():
         base = statistics.median(times[keys[0]])
         for kk, t in zip(keys, a.tags):
             md = statistics.median(times[kk])
-            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what in ("attn", "fwdlse", "bwd", "mlbwd") else ""
+            extra = f" {fl / md / 1e9:.0f} TF/s" if a.what in ("attn", "fwdlse", "bwd", "mlbwd", "mlattn") else ""
             print(f"{variant} {a.what} {kk}: median {md:.4f} ms (min {min(times[kk]):.4f}){extra}  "
                   f"x{base / md:.3f} vs {a.tags[0]}", flush=True)
 

@@ -1033,10 +1033,12 @@ static int launch_prep(const PrepParams& pp, hipStream_t s) {
   return check_launch("bwd_prep_kernel");
 }
 
+// kernel choice: vb_attn_bwd_args.kernel_select (VB_BWD_SEL_* bits); `ran` collects VB_BWD_RAN_* bits
 template <int D, class T>
-static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
+static int launch_grads(const BwdParams& p, bool pool, hipStream_t s, int sel, int& ran) {
   const int BH = p.B * p.H;
-  const bool pipe = dkdv_pipe_enabled(D);
+  const bool pipe = !(sel & VB_BWD_SEL_DKDV_ROUND3);
+  if ((pool && p.dkp) || p.k) ran |= pipe ? VB_BWD_RAN_DKDV_PIPE : VB_BWD_RAN_DKDV_ROUND3;
   constexpr bool kF16 = std::is_same<T, F16>::value;
   if (pool && p.dkp) {
     if (pipe) {
@@ -1060,7 +1062,8 @@ static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
       if (int rc = check_launch("bwd_dkdv_kernel")) return rc;
     }
   }
-  if (dq_pipe_enabled(D)) return launch_dq_pipe(p, D, pool, kF16, s);
+  if (!(sel & VB_BWD_SEL_DQ_ROUND3)) return launch_dq_pipe(p, D, pool, kF16, s, sel, ran);
+  ran |= VB_BWD_RAN_DQ_ROUND3;
   if (pool)
     hipLaunchKernelGGL((bwd_dq_kernel<D, T, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
   else
@@ -1068,15 +1071,18 @@ static int launch_grads(const BwdParams& p, bool pool, hipStream_t s) {
   return check_launch("bwd_dq_kernel");
 }
 
-static int dispatch_bwd(const PrepParams& pp, const BwdParams& p, int D, int dtype, bool pool, hipStream_t s) {
+static int dispatch_bwd(const PrepParams& pp, const BwdParams& p, int D, int dtype, bool pool, hipStream_t s,
+                        int sel = 0, int32_t* ran_out = nullptr) {
+  int ran = 0, rc;
   if (dtype == VB_DTYPE_BF16) {
-    if (int rc = launch_prep<BF16>(pp, s)) return rc;
-    if (D == 64) return launch_grads<64, BF16>(p, pool, s);
-    return launch_grads<128, BF16>(p, pool, s);
+    rc = launch_prep<BF16>(pp, s);
+    if (!rc) rc = D == 64 ? launch_grads<64, BF16>(p, pool, s, sel, ran) : launch_grads<128, BF16>(p, pool, s, sel, ran);
+  } else {
+    rc = launch_prep<F16>(pp, s);
+    if (!rc) rc = D == 64 ? launch_grads<64, F16>(p, pool, s, sel, ran) : launch_grads<128, F16>(p, pool, s, sel, ran);
   }
-  if (int rc = launch_prep<F16>(pp, s)) return rc;
-  if (D == 64) return launch_grads<64, F16>(p, pool, s);
-  return launch_grads<128, F16>(p, pool, s);
+  if (ran_out) *ran_out = ran;
+  return rc;
 }
 
 struct WsLayout {
@@ -1144,6 +1150,8 @@ extern "C" int vb_attn_bwd(const vb_attn_bwd_args* a, void* stream) {
   if (a->dtype != VB_DTYPE_BF16 && a->dtype != VB_DTYPE_F16) return fail(VB_ERR_INVALID, "vb_attn_bwd: unknown dtype");
   if (!a->q || !a->k || !a->v || !a->out || !a->lse || !a->dout || !a->dq || !a->dk || !a->dv)
     return fail(VB_ERR_INVALID, "vb_attn_bwd: missing tensor");
+  if (a->kernel_select & ~(VB_BWD_SEL_DKDV_ROUND3 | VB_BWD_SEL_DQ_ROUND3 | VB_BWD_SEL_DQ_RING4))
+    return fail(VB_ERR_INVALID, "vb_attn_bwd: unknown kernel_select bits");
   const bool pool = a->kp != nullptr;
   if (pool && (!a->vp || a->Lkp <= 0 || !a->out2 || !a->lse2 || a->pool_gap <= 0))
     return fail(VB_ERR_INVALID, "vb_attn_bwd: pooled branch needs vp, Lkp, out2, lse2 and pool_gap");
@@ -1219,7 +1227,8 @@ extern "C" int vb_attn_bwd(const vb_attn_bwd_args* a, void* stream) {
   p.scale = a->scale > 0.f ? a->scale : (float)(1.0 / sqrt((double)a->D));
   p.c = p.scale * kLog2e;
   p.heavy_rows = a->heavy_rows;
-  return dispatch_bwd(pp, p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream));
+  return dispatch_bwd(pp, p, a->D, a->dtype, pool, reinterpret_cast<hipStream_t>(stream), a->kernel_select,
+                      a->kernels_ran);
 }
 
 extern "C" uint64_t vb_block_sparse_attn_bwd_workspace_size(int batch, int num_heads, int max_seqlen_q) {
@@ -1318,8 +1327,9 @@ static MlWs ml_ws_layout(int B, int H, int L, int D, bool copies) {
 }
 
 template <int D, class T>
-static int launch_ml_grads(const PrepParams& pp, const BwdParams& p, hipStream_t s) {
+static int launch_ml_grads(const PrepParams& pp, const BwdParams& p, hipStream_t s, int sel, int& ran) {
   if (int rc = launch_prep<T>(pp, s)) return rc;
+  ran |= VB_BWD_RAN_ML_PYRAMID;
   const int BH = p.B * p.H;
   {
     constexpr int kW = D == 64 ? VB_ML_PYR_WAVES : 4, kRows = 32 * kW;   // items of kRows pyramid rows
@@ -1328,13 +1338,19 @@ static int launch_ml_grads(const PrepParams& pp, const BwdParams& p, hipStream_t
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, true, true, kW>), dim3(items * BH), dim3(kW * 64), 0, s, p);
   }
   if (int rc = check_launch("bwd_dkdv_kernel<multi-level pooled>")) return rc;
-  if (ml_dkdv_pipe_enabled()) {
+  if (!(sel & VB_BWD_SEL_DKDV_ROUND3)) {
+    ran |= VB_BWD_RAN_DKDV_PIPE;
     if (int rc = launch_ml_dkdv_pipe(p, D, std::is_same<T, F16>::value, s)) return rc;
   } else {
+    ran |= VB_BWD_RAN_DKDV_ROUND3;
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, T, false, true>), dim3(p.nbk * BH), dim3(bwd::kThreads), 0, s, p);
     if (int rc = check_launch("bwd_dkdv_kernel<multi-level>")) return rc;
   }
-  if (ml_dq_pipe_enabled()) return launch_ml_dq_pipe(p, D, std::is_same<T, F16>::value, s);
+  if (!(sel & VB_BWD_SEL_DQ_ROUND3)) {
+    ran |= VB_BWD_RAN_DQ_PIPE_RING2;
+    return launch_ml_dq_pipe(p, D, std::is_same<T, F16>::value, s);
+  }
+  ran |= VB_BWD_RAN_DQ_ROUND3;
   hipLaunchKernelGGL((bwd_dq_kernel<D, T, false, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
   return check_launch("bwd_dq_kernel<multi-level>");
 }
@@ -1354,6 +1370,8 @@ extern "C" int vb_ml_attn_bwd(const vb_ml_attn_bwd_args* a, void* stream) {
   if (a->dtype != VB_DTYPE_BF16 && a->dtype != VB_DTYPE_F16) return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: unknown dtype");
   if (!a->q || !a->kpyr || !a->vpyr || !a->level_mask || !a->out || !a->lse || !a->dout || !a->dq || !a->dk || !a->dv)
     return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: missing tensor");
+  if (a->kernel_select & ~(VB_BWD_SEL_DKDV_ROUND3 | VB_BWD_SEL_DQ_ROUND3))
+    return fail(VB_ERR_INVALID, "vb_ml_attn_bwd: unsupported kernel_select bits (the multi-level dQ has one ring)");
   const int nb = (a->L + 127) / 128;
   if (nb > bwd::kMaxBlocks) return fail(VB_ERR_UNSUPPORTED, "vb_ml_attn_bwd: sequence too long");
   const int64_t* strides[] = {a->q_stride, a->out_stride, a->dout_stride, a->dq_stride, a->dk_stride, a->dv_stride};
@@ -1416,7 +1434,12 @@ extern "C" int vb_ml_attn_bwd(const vb_ml_attn_bwd_args* a, void* stream) {
   p.c = p.scale * kLog2e;
   p.heavy_rows = a->heavy_rows;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int sel = a->kernel_select;
+  int ran = 0, rc;
   if (a->dtype == VB_DTYPE_BF16)
-    return a->D == 64 ? launch_ml_grads<64, BF16>(pp, p, st) : launch_ml_grads<128, BF16>(pp, p, st);
-  return a->D == 64 ? launch_ml_grads<64, F16>(pp, p, st) : launch_ml_grads<128, F16>(pp, p, st);
+    rc = a->D == 64 ? launch_ml_grads<64, BF16>(pp, p, st, sel, ran) : launch_ml_grads<128, BF16>(pp, p, st, sel, ran);
+  else
+    rc = a->D == 64 ? launch_ml_grads<64, F16>(pp, p, st, sel, ran) : launch_ml_grads<128, F16>(pp, p, st, sel, ran);
+  if (a->kernels_ran) *a->kernels_ran = ran;
+  return rc;
 }

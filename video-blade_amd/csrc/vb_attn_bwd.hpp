@@ -67,17 +67,12 @@ struct MlGeom {
 // The hand-scheduled dK/dV kernels (vb_attn_bwd_kv.hip): returns 0 or a VB_ERR code. `pooled`
 // selects the pooled-key pass (grid nbkp * B*H * psplit) over the full-resolution one (grid nbk * B*H).
 int launch_dkdv_pipe(const BwdParams& p, int D, bool pooled, bool f16, hipStream_t s);
-// env VB_BWD_KV128 / VB_BWD_KV64 (defaults VB_BWD_KV128_DEFAULT / VB_BWD_KV64_DEFAULT): route the
-// head dim's dK/dV to those kernels
-bool dkdv_pipe_enabled(int D);
-// the hand-scheduled dQ kernels (same file; grid nbq * B*H), env VB_BWD_DQ128 / VB_BWD_DQ64
-int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s);
-// the multi-level dQ on the 2-slot pipeline (vb_ml_attn_bwd); ml_dq_pipe_enabled() reads VB_BWD_MLDQ once
+// the hand-scheduled dQ kernels (same file; grid nbq * B*H) on the ring `sel` picks
+// (VB_BWD_SEL_DQ_RING4); ORs the VB_BWD_RAN_* bit of what it launched into `ran`
+int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s, int sel, int& ran);
+// the multi-level dQ on the 2-slot pipeline (vb_ml_attn_bwd)
 int launch_ml_dq_pipe(const BwdParams& p, int D, bool f16, hipStream_t s);
-bool ml_dq_pipe_enabled();
-// the multi-level level-1 dK/dV on the pipeline kernel (VB_BWD_MLKV, read once)
+// the multi-level level-1 dK/dV on the pipeline kernel
 int launch_ml_dkdv_pipe(const BwdParams& p, int D, bool f16, hipStream_t s);
-bool ml_dkdv_pipe_enabled();
-bool dq_pipe_enabled(int D);
 
 }  // namespace vb

@@ -27,14 +27,8 @@
 
 #include "vb_attn_bwd.hpp"
 
-#ifndef VB_BWD_KV128_DEFAULT
-#define VB_BWD_KV128_DEFAULT 1
-#endif
 #ifndef VB_KV64_WAVES
 #define VB_KV64_WAVES 1    // waves per SIMD the D=64 kernel is register-budgeted for (2 spills)
-#endif
-#ifndef VB_BWD_DQ128_DEFAULT
-#define VB_BWD_DQ128_DEFAULT 1
 #endif
 #ifndef VB_BWD_DQ128_RING
 // ring slots of the D=128 dQ pipeline: 2 (two workgroups per CU; Wan backward 1.073x over the
@@ -51,12 +45,6 @@
 #endif
 #ifndef VB_DQ64_R2_WGS
 #define VB_DQ64_R2_WGS 2     // workgroups per CU the D=64 2-slot form is register-budgeted for (3: 1.005x)
-#endif
-#ifndef VB_BWD_DQ64_DEFAULT
-#define VB_BWD_DQ64_DEFAULT 1
-#endif
-#ifndef VB_BWD_KV64_DEFAULT
-#define VB_BWD_KV64_DEFAULT 1
 #endif
 #ifndef VB_KV128_LA
 #define VB_KV128_LA 4      // operand lookahead in MFMAs
@@ -1517,18 +1505,6 @@ __global__ void __launch_bounds__(bwd::kThreads, R == 2 ? (D == 128 ? (kML ? 1 :
     }
 }
 
-// Kernel selection is read from the environment once per process (A/B switches), not per launch.
-static bool env_switch(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return (e ? atoi(e) : dflt) != 0;
-}
-
-bool dkdv_pipe_enabled(int D) {
-  static const bool on64 = env_switch("VB_BWD_KV64", VB_BWD_KV64_DEFAULT);
-  static const bool on128 = env_switch("VB_BWD_KV128", VB_BWD_KV128_DEFAULT);
-  return D == 128 ? on128 : on64;
-}
-
 template <int D>
 static int launch_pipe(const BwdParams& p, bool pooled, bool f16, hipStream_t s) {
   const int BH = p.B * p.H;
@@ -1544,12 +1520,6 @@ static int launch_pipe(const BwdParams& p, bool pooled, bool f16, hipStream_t s)
   return check_launch("bwd_dkdv_pipe_kernel");
 }
 
-bool dq_pipe_enabled(int D) {
-  static const bool on64 = env_switch("VB_BWD_DQ64", VB_BWD_DQ64_DEFAULT);
-  static const bool on128 = env_switch("VB_BWD_DQ128", VB_BWD_DQ128_DEFAULT);
-  return D == 128 ? on128 : on64;
-}
-
 template <int D, int R>
 static int launch_dq(const BwdParams& p, bool pool, bool f16, hipStream_t s) {
   const dim3 grid(p.nbq * p.B * p.H);
@@ -1563,34 +1533,14 @@ static int launch_dq(const BwdParams& p, bool pool, bool f16, hipStream_t s) {
   return check_launch("bwd_dq_pipe_kernel");
 }
 
-// D=128: the ring of VB_BWD_DQ128_RING slots (VB_BWD_DQ128_RING=2|4 in the environment)
-static int dq128_ring() {
-  static const int r = [] {
-    const char* e = getenv("VB_BWD_DQ128_RING");
-    return (e ? atoi(e) : VB_BWD_DQ128_RING) == 2 ? 2 : 4;
-  }();
-  return r;
+// ring slots: VB_BWD_DQ{64,128}_RING by default, 4 with VB_BWD_SEL_DQ_RING4
+int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s, int sel, int& ran) {
+  const bool ring4 = (sel & VB_BWD_SEL_DQ_RING4) || (D == 64 ? VB_BWD_DQ64_RING : VB_BWD_DQ128_RING) != 2;
+  ran |= ring4 ? VB_BWD_RAN_DQ_PIPE_RING4 : VB_BWD_RAN_DQ_PIPE_RING2;
+  if (D == 64) return ring4 ? launch_dq<64, 4>(p, pool, f16, s) : launch_dq<64, 2>(p, pool, f16, s);
+  return ring4 ? launch_dq<128, 4>(p, pool, f16, s) : launch_dq<128, 2>(p, pool, f16, s);
 }
 
-int launch_dq_pipe(const BwdParams& p, int D, bool pool, bool f16, hipStream_t s) {
-  if (D == 64) return VB_BWD_DQ64_RING == 2 ? launch_dq<64, 2>(p, pool, f16, s) : launch_dq<64, 4>(p, pool, f16, s);
-  return dq128_ring() == 2 ? launch_dq<128, 2>(p, pool, f16, s) : launch_dq<128, 4>(p, pool, f16, s);
-}
-
-#ifndef VB_BWD_MLDQ_DEFAULT
-#define VB_BWD_MLDQ_DEFAULT 1
-#endif
-bool ml_dq_pipe_enabled() {
-  static const bool on = env_switch("VB_BWD_MLDQ", VB_BWD_MLDQ_DEFAULT);
-  return on;
-}
-#ifndef VB_BWD_MLKV_DEFAULT
-#define VB_BWD_MLKV_DEFAULT 1
-#endif
-bool ml_dkdv_pipe_enabled() {
-  static const bool on = env_switch("VB_BWD_MLKV", VB_BWD_MLKV_DEFAULT);
-  return on;
-}
 int launch_ml_dkdv_pipe(const BwdParams& p, int D, bool f16, hipStream_t s) {
   const dim3 grid(p.nbk * p.B * p.H);
   if (D == 128) {

@@ -19,6 +19,7 @@
 //                                        the S^T accumulator registers (no LDS round trip)
 // Gilbert reorder: q/k/v rows are gathered through q_rows / kv_rows and O/LSE scattered through
 // q_rows, so the reference's index_select + cat + reverse (:141-161) cost no pass of their own.
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -30,8 +31,8 @@
 #endif
 #if VB_ATTN_TRACE
 namespace vb { __device__ TraceBuf g_attn_trace; }
-#define VB_ATRACE_START(k) trace_start(g_attn_trace, k)
-#define VB_ATRACE_END() trace_end(g_attn_trace)
+#define VB_ATRACE_START(k) trace_start(g_attn_trace, k, (unsigned)vblk)
+#define VB_ATRACE_END() trace_end(g_attn_trace, (unsigned)vblk)
 #else
 #define VB_ATRACE_START(k)
 #define VB_ATRACE_END()
@@ -67,8 +68,41 @@ __device__ __forceinline__ unsigned long long vb_stamp() {
 #define VB_ACC(i, d)
 #endif
 
-template <int D, class T, bool kPool, bool kKvRows, bool kML = false, bool kCBias = false>
-__global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) attn_fwd_kernel(const FwdParams p) {
+// LDS of one attention workgroup: the K/V ring, the kept-block list and its count, and (gathered
+// K/V) the kv_rows entry ring
+template <int D, bool kKvRows>
+constexpr int fwd_smem_bytes() {
+  return ((D == 64) ? 3 : 2) * 2 * kKT * D * 2 + kMaxBlocks * 2 + 16 + (kKvRows ? 4 * 512 : 0);
+}
+
+// Persistent dispatch (vb_attn_args.work_queue): the launch is resident-sized and every workgroup
+// pulls work items from per-XCD queue heads. Item v (a "virtual blockIdx" in [0, total)) belongs to
+// queue v % 8, in increasing v: the same items, in the same per-XCD order, as one workgroup per item
+// dealt round-robin over the XCDs. A workgroup drains its own XCD's queue (w % 8 shares an XCD, like
+// blockIdx % 8 of the one-per-item grid), then takes the remaining items of the other queues, so no
+// XCD idles while another still has work. Heads are 128 bytes apart; wq[kWqDone] counts finished
+// workgroups and the last one to finish zeroes every word, so each launch finds the queue at zero
+// (the buffer is zero before its first use).
+constexpr int kWqStride = 32;
+constexpr int kWqDone = 8 * kWqStride;
+__device__ __forceinline__ int wq_fetch(int* wq, int home, int total) {
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    const int x = (home + i) & 7;
+    const int cnt = (total - x + 7) >> 3;   // items x, x + 8, x + 16, ...
+    if (cnt > 0) {
+      const int j = __hip_atomic_fetch_add(wq + x * kWqStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (j < cnt) return x + 8 * j;
+    }
+  }
+  return -1;
+}
+
+// One work item: the (b, h, 128-row q-block) of virtual blockIdx `vblk`. With a work queue, lane 0
+// of wave 0 claims the workgroup's next item at the start of the item's last tile (`next`), so the
+// claim's round trip overlaps that tile and the epilogue.
+template <int D, class T, bool kPool, bool kKvRows, bool kML, bool kCBias>
+__device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk, uint8_t* smem, int& next) {
   constexpr int KS = D / 16;                   // k-steps of the QK^T product
   constexpr int DT = D / 32;                   // 32-wide d tiles of the output
   constexpr bool kSplitPV = VB_FWD_SPLIT_PV && D == 64;   // measured: +0.8 % at D=64, -1.4 % at D=128
@@ -91,13 +125,17 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   constexpr int kRowsPerInst = 1024 / kRowB;   // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerMat = kMatBytes / 1024;
   constexpr int kInstPerWave = 2 * kInstPerMat / 4;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kBufs * kBufBytes + kMaxBlocks * 2 + 16 + (kKvRows ? 4 * 512 : 0)];
+  static_assert(fwd_smem_bytes<D, kKvRows>() == kBufs * kBufBytes + kMaxBlocks * 2 + 16 + (kKvRows ? 4 * 512 : 0), "LDS layout");
   static_assert(!(kML && (kPool || kKvRows)), "multi-level mode reads the KV pyramids only");
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
   int* list_n = reinterpret_cast<int*>(smem + kBufs * kBufBytes + kMaxBlocks * 2);
 
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // The thread id is laundered per item: otherwise the persistent loop hoists every lane-derived
+  // address (DMA chunks, LDS fragment bases) out of the item loop and spills them across it.
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   const int half = lane >> 5;
   const int l32 = lane & 31;
@@ -114,12 +152,12 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   const int hr = min(p.heavy_rows, p.nbq);
   const int n_heavy = hr * BH;
   int qblk, bh;
-  if ((int)blockIdx.x < n_heavy) {
-    qblk = p.nbq - 1 - (int)(blockIdx.x / BH);
-    bh = blockIdx.x % BH;
+  if (vblk < n_heavy) {
+    qblk = p.nbq - 1 - vblk / BH;
+    bh = vblk % BH;
   } else {
     const int rows_left = p.nbq - hr;
-    int lin = xcd_linear(blockIdx.x - n_heavy, rows_left * BH);
+    int lin = xcd_linear(vblk - n_heavy, rows_left * BH);
     if (p.q_order) lin = __builtin_amdgcn_readfirstlane(p.q_order[lin]);   // longest first (attn_order_kernel)
     bh = lin / rows_left;
     qblk = rows_left - 1 - lin % rows_left;
@@ -152,7 +190,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   if (kML) {
     // multi-level: per-level lists of key blocks (levels 1, 2, 4, 8, in that order), built in two
     // passes over the mask row (counts, then positions) so they share the one kMaxBlocks array
-    if (threadIdx.x < 64) {
+    if (tid < 64) {
       int cnt[4] = {0, 0, 0, 0};
       for (int j0 = 0; j0 < nbk; j0 += 64) {
         const int j = j0 + lane;
@@ -175,7 +213,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
       }
       if (lane < 4) list_n[lane] = cnt[0] * (lane == 0) + cnt[1] * (lane == 1) + cnt[2] * (lane == 2) + cnt[3] * (lane == 3);
     }
-  } else if (threadIdx.x < 64) {
+  } else if (tid < 64) {
     int n = 0;
     int dpos = -1;   // list position of the diagonal block (key block qblk), if kept
     if (p.use_main) {
@@ -914,6 +952,8 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     VB_ACC(2, st3 - st2);
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
+    if (p.work_queue && t0 + kBufs >= ntiles && tid == 0)   // the last ring round: claim the next item
+      next = wq_fetch(p.work_queue, blockIdx.x & 7, p.n_items);
     body(t0, std::integral_constant<int, 0>{});
     if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
     if constexpr (kBufs > 2)
@@ -970,6 +1010,35 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
   VB_ATRACE_END();
 }
 
+template <int D, class T, bool kPool, bool kKvRows, bool kML = false, bool kCBias = false>
+__global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) attn_fwd_kernel(const FwdParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[fwd_smem_bytes<D, kKvRows>()];
+  __shared__ int next_s;
+  int* const wq = p.work_queue;
+  int item = blockIdx.x;
+  if (wq) {   // persistent: the first item from the queue too (the grid is resident-sized)
+    if (threadIdx.x == 0) next_s = wq_fetch(wq, blockIdx.x & 7, p.n_items);
+    __syncthreads();
+    item = next_s;
+  }
+  while (item >= 0) {
+    int next = -2;   // -2: not claimed during the item (it had no tile)
+    attn_fwd_item<D, T, kPool, kKvRows, kML, kCBias>(p, item, smem, next);
+    if (!wq) break;
+    // every wave is done with this item's LDS (ring, list) before the next item's prologue writes it
+    if (threadIdx.x == 0) next_s = next == -2 ? wq_fetch(wq, blockIdx.x & 7, p.n_items) : next;
+    __syncthreads();
+    item = next_s;
+    __syncthreads();   // next_s is read by every wave before lane 0 may overwrite it
+  }
+  if (wq && threadIdx.x == 0) {
+    // the last workgroup to finish (all fetches of every workgroup have returned) re-zeroes the queue
+    const int done = __hip_atomic_fetch_add(wq + kWqDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == (int)gridDim.x - 1)
+      for (int x = 0; x <= 8; ++x) __hip_atomic_store(wq + x * kWqStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Dispatch order of the attention kernel's phase 2 (longest-processing-time first, per XCD): the
 // kernel deals workgroups round-robin over the 8 XCDs and gives XCD x the contiguous range of
 // linear work items xcd_linear assigns it (head-major). Each XCD drains its range in order, so its
@@ -998,11 +1067,12 @@ __global__ void __launch_bounds__(1024) attn_order_kernel(const FwdParams p, int
   const int bh0 = start / rows_left;
   const int nh = (start + count - 1) / rows_left - bh0 + 1;
   const int nl = p.nbk + 1;   // kept counts 0..nbk
-  if ((int64_t)nh * nl > kOrderBins) {   // too many bins for LDS: keep the kernel's own order
-    for (int i = threadIdx.x; i < count; i += blockDim.x) order[start + i] = start + i;
-    return;
-  }
-  for (int i = threadIdx.x; i < nh * nl; i += blockDim.x) bins[i] = 0;
+  // (head, length) bins; a range spanning more heads than LDS has bins for sorts by length alone
+  // (longest first over the whole range: the tail is still the shortest items, the head-major
+  // grouping is given up). nl <= kMaxBlocks + 1 < kOrderBins always fits.
+  const bool by_head = (int64_t)nh * nl <= kOrderBins;
+  const int nbins = by_head ? nh * nl : nl;
+  for (int i = threadIdx.x; i < nbins; i += blockDim.x) bins[i] = 0;
   __syncthreads();
   auto key_of = [&](int lin) -> int {
     const int bh = lin / rows_left, qblk = rows_left - 1 - lin % rows_left;
@@ -1016,13 +1086,12 @@ __global__ void __launch_bounds__(1024) attn_order_kernel(const FwdParams p, int
       kept = 0;
       for (int j = 0; j < p.nbk; ++j) kept += mrow[j] != 0;
     }
-    return (bh - bh0) * nl + (p.nbk - kept);   // head ascending, kept count descending
+    return (by_head ? (bh - bh0) * nl : 0) + (p.nbk - kept);   // head ascending, kept count descending
   };
   for (int i = threadIdx.x; i < count; i += blockDim.x) atomicAdd(&bins[key_of(start + i)], 1);
   __syncthreads();
   {   // exclusive prefix over the bins: every thread a run of C bins, a scan of the runs' sums
     __shared__ int wsum[16];
-    const int nbins = nh * nl;
     const int C = (nbins + 1023) / 1024;
     const int b0 = threadIdx.x * C;
     int run = 0;
@@ -1053,28 +1122,48 @@ __global__ void __launch_bounds__(1024) attn_order_kernel(const FwdParams p, int
   }
 }
 
+// Grid of one launch: one workgroup per item, or (work queue) as many as are resident at once —
+// the occupancy of this instantiation times the device's CUs (host queries, cached per kernel and
+// device; no device synchronisation), a multiple of 8 so every XCD gets the same number.
+template <auto Kern>
+static unsigned fwd_grid(FwdParams& p) {
+  const unsigned items = (unsigned)(p.nbq * p.B * p.H);
+  p.n_items = (int)items;
+  if (!p.work_queue) return items;
+  static std::atomic<int> slots_by_dev[64];   // 0 = not queried yet
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int slots = slots_by_dev[dev].load(std::memory_order_relaxed);
+  if (slots == 0) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, Kern, kThreads, 0) != hipSuccess) per_cu = 0;
+    slots = cus * per_cu > 8 ? cus * per_cu / 8 * 8 : 8;
+    slots_by_dev[dev].store(slots, std::memory_order_relaxed);
+  }
+  return (unsigned)slots < items ? (unsigned)slots : items;
+}
+
+template <auto Kern>
+static int launch_one(FwdParams p, hipStream_t stream, const char* what) {
+  const unsigned grid = fwd_grid<Kern>(p);
+  hipLaunchKernelGGL(Kern, dim3(grid), dim3(kThreads), 0, stream, p);
+  return check_launch(what);
+}
+
 template <int D, class T>
 static int launch_fwd(const FwdParams& p, bool pool, hipStream_t stream) {
-  const dim3 grid(p.nbq * p.B * p.H);
   const bool rows = p.kv_rows != nullptr;
   const bool cbias = VB_FWD_CBIAS && p.lse == nullptr;
-  if (cbias && pool && rows)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, true, false, true>), grid, dim3(kThreads), 0, stream, p);
-  else if (cbias && rows)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, true, false, true>), grid, dim3(kThreads), 0, stream, p);
-  else if (cbias && pool)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, false, false, true>), grid, dim3(kThreads), 0, stream, p);
-  else if (cbias)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, false, false, true>), grid, dim3(kThreads), 0, stream, p);
-  else if (pool && rows)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, true>), grid, dim3(kThreads), 0, stream, p);
-  else if (pool)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, true, false>), grid, dim3(kThreads), 0, stream, p);
-  else if (rows)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, true>), grid, dim3(kThreads), 0, stream, p);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<D, T, false, false>), grid, dim3(kThreads), 0, stream, p);
-  return check_launch("attn_fwd_kernel");
+  const char* w = "attn_fwd_kernel";
+  if (cbias && pool && rows) return launch_one<attn_fwd_kernel<D, T, true, true, false, true>>(p, stream, w);
+  if (cbias && rows) return launch_one<attn_fwd_kernel<D, T, false, true, false, true>>(p, stream, w);
+  if (cbias && pool) return launch_one<attn_fwd_kernel<D, T, true, false, false, true>>(p, stream, w);
+  if (cbias) return launch_one<attn_fwd_kernel<D, T, false, false, false, true>>(p, stream, w);
+  if (pool && rows) return launch_one<attn_fwd_kernel<D, T, true, true>>(p, stream, w);
+  if (pool) return launch_one<attn_fwd_kernel<D, T, true, false>>(p, stream, w);
+  if (rows) return launch_one<attn_fwd_kernel<D, T, false, true>>(p, stream, w);
+  return launch_one<attn_fwd_kernel<D, T, false, false>>(p, stream, w);
 }
 
 static int dispatch_fwd(const FwdParams& p, int D, int dtype, bool pool, hipStream_t stream) {
@@ -1162,6 +1251,7 @@ extern "C" int vb_attn_fwd(const vb_attn_args* a, void* stream) {
 #endif
   p.q_len = a->q_lengths;
   p.order_window = a->order_window;
+  p.work_queue = a->work_queue;
   if (a->q_order && p.use_main && p.mask) {   // longest-first dispatch order (scheduling only)
     hipLaunchKernelGGL(attn_order_kernel, dim3(8), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), p,
                        a->q_order);
@@ -1215,23 +1305,23 @@ extern "C" int vb_ml_attn_fwd(const vb_ml_attn_args* a, void* stream) {
   const float scale = a->scale > 0.f ? a->scale : (float)(1.0 / sqrt((double)a->D));
   p.c = scale * kLog2e;
   p.heavy_rows = a->heavy_rows;
-  const dim3 grid(p.nbq * p.B * p.H);
+  p.work_queue = a->work_queue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool cb = VB_FWD_CBIAS && p.lse == nullptr;   // inference launches (see kCBias)
+  const char* w = "attn_fwd_kernel (multi-level)";
   if (a->dtype == VB_DTYPE_BF16) {
-    if (a->D == 64 && cb) hipLaunchKernelGGL((attn_fwd_kernel<64, BF16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
-    else if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, BF16, false, false, true>), grid, dim3(kThreads), 0, st, p);
-    else if (cb) hipLaunchKernelGGL((attn_fwd_kernel<128, BF16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
-    else hipLaunchKernelGGL((attn_fwd_kernel<128, BF16, false, false, true>), grid, dim3(kThreads), 0, st, p);
-  } else if (a->dtype == VB_DTYPE_F16) {
-    if (a->D == 64 && cb) hipLaunchKernelGGL((attn_fwd_kernel<64, F16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
-    else if (a->D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, F16, false, false, true>), grid, dim3(kThreads), 0, st, p);
-    else if (cb) hipLaunchKernelGGL((attn_fwd_kernel<128, F16, false, false, true, true>), grid, dim3(kThreads), 0, st, p);
-    else hipLaunchKernelGGL((attn_fwd_kernel<128, F16, false, false, true>), grid, dim3(kThreads), 0, st, p);
-  } else {
-    return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: unknown dtype");
+    if (a->D == 64 && cb) return launch_one<attn_fwd_kernel<64, BF16, false, false, true, true>>(p, st, w);
+    if (a->D == 64) return launch_one<attn_fwd_kernel<64, BF16, false, false, true>>(p, st, w);
+    if (cb) return launch_one<attn_fwd_kernel<128, BF16, false, false, true, true>>(p, st, w);
+    return launch_one<attn_fwd_kernel<128, BF16, false, false, true>>(p, st, w);
   }
-  return check_launch("attn_fwd_kernel (multi-level)");
+  if (a->dtype == VB_DTYPE_F16) {
+    if (a->D == 64 && cb) return launch_one<attn_fwd_kernel<64, F16, false, false, true, true>>(p, st, w);
+    if (a->D == 64) return launch_one<attn_fwd_kernel<64, F16, false, false, true>>(p, st, w);
+    if (cb) return launch_one<attn_fwd_kernel<128, F16, false, false, true, true>>(p, st, w);
+    return launch_one<attn_fwd_kernel<128, F16, false, false, true>>(p, st, w);
+  }
+  return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: unknown dtype");
 }
 
 extern "C" int vb_block_sparse_attn_fwd(const void* q_unpad, const void* k_unpad, const void* v_unpad,

@@ -27,6 +27,8 @@ struct FwdParams {
   int Lpad;                                   // level-1 rows (ceil(L/128)*128)
   int ref_tail;                               // 1: level-1 tail keys >= L take part (zero rows)
   int dbg;                                    // diagnostic builds only (VB_DEBUG_ATTN)
+  int* work_queue;                            // persistent dispatch: per-XCD queue heads, or NULL
+  int n_items;                                // work items (nbq * B * H) behind the queue
 };
 
 #ifndef VB_DIAG

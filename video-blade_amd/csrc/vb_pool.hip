@@ -16,12 +16,9 @@ __global__ void __launch_bounds__(256) pool_kv_kernel(const PoolTask t) {
 
 // Workgroups of an HBM-bound pass that runs beside the predictor's score kernel on another stream:
 // a capped, grid-strided launch leaves most CUs to the MFMA-bound kernel instead of flooding the
-// dispatcher (VB_POOL_WGS overrides; 0 = one workgroup per 256 chunks).
+// dispatcher (the build's VB_POOL_WGS_DEFAULT; 0 = one workgroup per 256 chunks).
 unsigned pool_grid(int64_t work_items) {
-  static const int cap = [] {
-    const char* e = getenv("VB_POOL_WGS");
-    return e ? atoi(e) : kPoolWgsDefault;
-  }();
+  constexpr int cap = kPoolWgsDefault;
   const int64_t n = (work_items + 255) / 256;
   return (unsigned)((cap > 0 && n > cap) ? cap : n);
 }

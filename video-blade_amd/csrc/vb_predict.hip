@@ -998,7 +998,10 @@ extern "C" int vb_mask_predict(const vb_predict_args* a, void* stream) {
   p.thr = a->energy_threshold;
   p.min_keep = a->min_keep; p.max_keep = a->max_keep; p.force_tail = a->force_tail;
   p.po = a->po; p.mask = a->mask; p.count = a->mask_count;
-  p.rows_kept = a->mask_level ? nullptr : a->mask_rows_kept;
+  // the kept counts come from the energy rule of the fused epilogue: refused where it does not run
+  if (a->mask_rows_kept && (a->mask_level || !a->mask || VB_PRED_SPLIT_ENERGY))
+    return fail(VB_ERR_INVALID, "vb_mask_predict: mask_rows_kept needs the energy mask (mask set, mask_level 0)");
+  p.rows_kept = a->mask_rows_kept;
   p.q_s = nullptr;
   p.k_s = reinterpret_cast<uint8_t*>(a->workspace);
   p.rbuf = reinterpret_cast<uint16_t*>(p.k_s + rows_b);

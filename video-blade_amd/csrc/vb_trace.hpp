@@ -23,22 +23,23 @@ __device__ __forceinline__ unsigned long long trace_clk() {
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
-__device__ __forceinline__ void trace_start(TraceBuf& b, int kind) {
-  if (blockIdx.x < kTraceWgs && threadIdx.x == 0) {
+// `row`: the workgroup's record (its blockIdx, or the work item a persistent workgroup is running)
+__device__ __forceinline__ void trace_start(TraceBuf& b, int kind, unsigned row = blockIdx.x) {
+  if (row < kTraceWgs && threadIdx.x == 0) {
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    b.v[blockIdx.x][0] = trace_now();
-    b.v[blockIdx.x][5] = hw;
-    b.v[blockIdx.x][6] = xcc;
-    b.v[blockIdx.x][7] = kind;
-    b.v[blockIdx.x][8] = trace_clk();
+    b.v[row][0] = trace_now();
+    b.v[row][5] = hw;
+    b.v[row][6] = xcc;
+    b.v[row][7] = kind;
+    b.v[row][8] = trace_clk();
   }
 }
-__device__ __forceinline__ void trace_end(TraceBuf& b) {
-  if (blockIdx.x < kTraceWgs && (threadIdx.x & 63) == 0) {
-    b.v[blockIdx.x][1 + (threadIdx.x >> 6)] = trace_now();
-    if (threadIdx.x == 0) b.v[blockIdx.x][9] = trace_clk();
+__device__ __forceinline__ void trace_end(TraceBuf& b, unsigned row = blockIdx.x) {
+  if (row < kTraceWgs && (threadIdx.x & 63) == 0) {
+    b.v[row][1 + (threadIdx.x >> 6)] = trace_now();
+    if (threadIdx.x == 0) b.v[row][9] = trace_clk();
   }
 }
 

@@ -38,6 +38,7 @@ class AttnArgs(ctypes.Structure):
         ("dtype", ctypes.c_int),
         ("heavy_rows", ctypes.c_int),
         ("q_order", _vp), ("q_lengths", _vp), ("order_window", ctypes.c_int),
+        ("work_queue", _vp),
     ]
 
 
@@ -89,6 +90,7 @@ class BwdArgs(ctypes.Structure):
         ("scale", ctypes.c_float),
         ("dtype", ctypes.c_int),
         ("heavy_rows", ctypes.c_int),
+        ("kernel_select", ctypes.c_int), ("kernels_ran", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 
@@ -106,6 +108,7 @@ class MlAttnArgs(ctypes.Structure):
         ("ref_tail", ctypes.c_int),
         ("dtype", ctypes.c_int),
         ("heavy_rows", ctypes.c_int),
+        ("work_queue", _vp),
     ]
 
 
@@ -127,8 +130,17 @@ class MlBwdArgs(ctypes.Structure):
         ("ref_tail", ctypes.c_int),
         ("dtype", ctypes.c_int),
         ("heavy_rows", ctypes.c_int),
+        ("kernel_select", ctypes.c_int), ("kernels_ran", ctypes.POINTER(ctypes.c_int32)),
     ]
 
+
+# vb_attn_bwd_args.kernel_select / kernels_ran bits (include/vblade.h)
+VB_BWD_SEL_DKDV_ROUND3, VB_BWD_SEL_DQ_ROUND3, VB_BWD_SEL_DQ_RING4 = 1, 2, 4
+VB_BWD_RAN_DKDV_PIPE, VB_BWD_RAN_DKDV_ROUND3 = 1, 2
+VB_BWD_RAN_DQ_PIPE_RING2, VB_BWD_RAN_DQ_PIPE_RING4, VB_BWD_RAN_DQ_ROUND3 = 4, 8, 16
+VB_BWD_RAN_ML_PYRAMID = 32
+VB_WORK_QUEUE_INTS = 288
+ABI_VERSION = 4
 
 # name -> (restype, argtypes); must list every symbol include/vblade.h declares
 SIGNATURES = {
@@ -198,7 +210,7 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.vb_abi_version() != 3:
+    if lib.vb_abi_version() != ABI_VERSION:
         raise VBladeError("libvblade_hip.so ABI version mismatch")
     _lib = lib
     return lib

@@ -46,6 +46,10 @@ VARIANT_DEFAULTS = {
 # Gilbert-neighbour order's L2 reuse and the extra launch cost more than the tail)
 ORDER_DEFAULT = {"cog": False, "wan": True}
 
+# persistent attention launch (resident-sized grid, per-XCD work queues; ops.attention_fwd
+# persistent=True), per variant
+PERSISTENT_DEFAULT = {"cog": True, "wan": True}
+
 
 def retain_counts(nb: int, min_ratio: float, max_ratio: float, variant: str):
     """Kept-block clamp bounds. cog: (seq * fp32 ratio tensor).to(int) clamped >= 1
@@ -130,7 +134,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
             raise ValueError(f"variant must be one of {list(VARIANT_DEFAULTS)}")
         cfg = dict(VARIANT_DEFAULTS[variant])
         unknown = set(overrides) - set(cfg) - {"energy_threshold", "block", "num_keep", "overlap", "gather_kv",
-                                               "mask_head_mode", "order", "order_window"}
+                                               "mask_head_mode", "order", "order_window", "persistent"}
         if unknown:
             raise TypeError(f"unknown options {sorted(unknown)}")
         cfg.update(overrides)
@@ -180,6 +184,11 @@ class AdaptiveBlockSparseAttn(nn.Module):
         # head-major Gilbert-neighbour order elsewhere for its L2 reuse.
         self.order = bool(cfg.get("order", ORDER_DEFAULT[variant]))
         self.order_window = int(cfg.get("order_window", 0))
+        # The fused attention launch is resident-sized (as many workgroups as fit on the device at
+        # once) and its workgroups pull q-blocks from per-XCD queues in the order above, then help
+        # the other XCDs: no per-workgroup launch gaps, no XCD left idle at the end. Scheduling
+        # only: outputs are bit-identical.
+        self.persistent = bool(cfg.get("persistent", PERSISTENT_DEFAULT[variant]))
 
     # -------------------------------------------------------------------------------- helpers
     def _rows(self, device):
@@ -330,7 +339,7 @@ class AdaptiveBlockSparseAttn(nn.Module):
             out = ops.attention_fwd(q, k_src, v_src, block_mask=mask, q_rows=rows, kv_rows=kv_rows,
                                     kp=kp, vp=vp, kp_log_bias=self._log_gap(q.dtype),
                                     heavy_rows=self.force_tail, order=self.order, q_lengths=rows_kept,
-                                    order_window=self.order_window)
+                                    order_window=self.order_window, persistent=self.persistent)
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()

@@ -132,9 +132,10 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
     include/vblade.h, vb_ml_attn_fwd)."""
 
     def __init__(self, *, mask_ratios=None, ref_tail: bool = True, log_every: int = 600,
-                 overlap: bool = True, **overrides):
+                 overlap: bool = True, persistent: bool = True, **overrides):
         """overlap: run the KV pyramid pass inside the predictor's launch (True) or as its own
-        launch after it."""
+        launch after it. persistent: the attention launch is resident-sized and pulls q-blocks
+        from per-XCD work queues (scheduling only; see attention.PERSISTENT_DEFAULT)."""
         super().__init__()
         cfg = dict(DEFAULTS)
         unknown = set(overrides) - set(cfg)
@@ -155,6 +156,7 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
         self.attn_event_every = 1
         self._attn_launches = 0
         self.overlap = bool(overlap)
+        self.persistent = bool(persistent)
 
     def _rows(self, device):
         if not self.use_rearrange:
@@ -207,7 +209,7 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
             out = ops.ml_attention_fwd(q, kpyr, vpyr, mask, q_rows=rows, ref_tail=self.ref_tail,
-                                       heavy_rows=2)
+                                       heavy_rows=2, persistent=self.persistent)
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()

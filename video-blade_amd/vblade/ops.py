@@ -63,6 +63,29 @@ def _aligned_bhld(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+_WORK_QUEUES = {}
+
+
+def work_queue(dev) -> torch.Tensor:
+    """The persistent forward's work queue (include/vblade.h VB_WORK_QUEUE_INTS) for ``dev``'s current
+    stream: int32, zero when allocated, and left zero by every launch that uses it. One per (device,
+    stream), since two launches that may overlap must not share one."""
+    dev = torch.device(dev)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, _stream(dev))
+    wq = _WORK_QUEUES.get(key)
+    if wq is None:
+        wq = _WORK_QUEUES[key] = torch.zeros(_lib.VB_WORK_QUEUE_INTS, device=dev, dtype=torch.int32)
+    return wq
+
+
+def _check_dev(name: str, t: torch.Tensor, dev):
+    """A pointer handed to a kernel must live on the launch's device (a CPU or other-GPU tensor
+    would be a device fault or a write to the wrong memory, not a Python error)."""
+    if t.device != dev:
+        raise ValueError(f"{name} must be on {dev}, got {t.device}")
+
+
 # ----------------------------------------------------------------------------------------------
 # Gilbert permutation
 # ----------------------------------------------------------------------------------------------
@@ -91,15 +114,17 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
                   scale: Optional[float] = None, need_lse: bool = False,
                   out: Optional[torch.Tensor] = None, heavy_rows: int = 0, order: bool = False,
                   q_lengths: Optional[torch.Tensor] = None, order_window: int = 0,
-                  q_order_out: Optional[torch.Tensor] = None):
+                  q_order_out: Optional[torch.Tensor] = None, persistent: bool = False):
     """vb_attn_fwd: softmax over (block-masked keys of k/v) ∪ (pooled keys kp/vp + bias).
     q,k,v [B,H,L,D]; block_mask [B,H,ceil(Lq/128),ceil(Lk/128)] bool/uint8; rows int32.
     ``order``: dispatch each XCD's q-blocks longest first (scheduling only; ``q_lengths`` [B,H,nbq]
     int32 kept blocks per mask row from mask_predict(rows_kept=...), else counted on the device;
     ``order_window`` > 0 re-orders only the last that many q-blocks of each XCD's range;
     ``q_order_out``: int32 [B*H*ceil(Lq/128)] to receive the dispatch permutation, for tests).
+    ``persistent``: a resident-sized launch whose workgroups pull q-blocks from per-XCD queues
+    (work_queue(); scheduling only, the same outputs).
     Returns out [B,H,Lq,D] (and lse fp32 [B,H,Lq] when need_lse)."""
-    dev = _require_gpu(q, k, v, block_mask, q_rows, kv_rows, kp, vp)
+    dev = _require_gpu(q, k, v, block_mask, q_rows, kv_rows, kp, vp, q_lengths, q_order_out)
     q = _aligned_bhld(q)
     B, H, Lq, D = q.shape
     if use_main:
@@ -143,6 +168,8 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
     a.scale = float(scale) if scale else 0.0
     a.dtype = _dtype_code(q)
     a.heavy_rows = int(heavy_rows)
+    if persistent:
+        a.work_queue = work_queue(dev).data_ptr()
     if order and block_mask is not None and use_main:
         nbq = (Lq + BLOCK - 1) // BLOCK
         q_order = q_order_out if q_order_out is not None else torch.empty(B * H * nbq, device=dev, dtype=torch.int32)
@@ -153,6 +180,7 @@ def attention_fwd(q: torch.Tensor, k: Optional[torch.Tensor], v: Optional[torch.
         if q_lengths is not None:
             if q_lengths.dtype != torch.int32 or q_lengths.numel() != B * H * nbq or not q_lengths.is_contiguous():
                 raise ValueError("attention_fwd: q_lengths must be contiguous int32 [B,H,ceil(Lq/128)]")
+            _check_dev("attention_fwd: q_lengths", q_lengths, dev)
             a.q_lengths = q_lengths.data_ptr()
     check(_lib.load().vb_attn_fwd(ctypes.byref(a), _stream(dev)), "vb_attn_fwd")
     return (out, lse) if need_lse else out
@@ -221,11 +249,14 @@ def _mask_u8(block_mask, Lq, Lk):
 
 def attention_bwd(dout, q, k, v, out, lse, *, block_mask=None, q_rows=None, kv_rows=None,
                   kp=None, vp=None, out2=None, lse2=None, alpha=None, gap: int = 0,
-                  scale: Optional[float] = None, heavy_rows: int = 0, dk_rows: Optional[int] = None):
+                  scale: Optional[float] = None, heavy_rows: int = 0, dk_rows: Optional[int] = None,
+                  kernel_select: int = 0, kernels_ran: Optional[list] = None):
     """vb_attn_bwd: gradients (dq, dk, dv) of the block-sparse attention, optionally of the
     adaptive two-branch form (kp/vp/out2/lse2/alpha/gap: alpha detached, pooled grads folded back
     through the mean pool). k/v hold keys in reordered order; dk/dv rows are written at
-    kv_rows[g] (dk_rows = number of rows of dk/dv, default Lk). Returns bf16/fp16 tensors."""
+    kv_rows[g] (dk_rows = number of rows of dk/dv, default Lk). Returns bf16/fp16 tensors.
+    ``kernel_select``: _lib.VB_BWD_SEL_* bits (0: the default kernels); ``kernels_ran`` (a list)
+    receives the _lib.VB_BWD_RAN_* bits of the kernels the call launched."""
     dev = _require_gpu(dout, q, k, v, out, lse, block_mask, q_rows, kv_rows, kp, vp, out2, lse2,
                        alpha)
     q, k, v, out, dout = (_aligned_bhld(t) for t in (q, k, v, out, dout))
@@ -262,11 +293,16 @@ def attention_bwd(dout, q, k, v, out, lse, *, block_mask=None, q_rows=None, kv_r
     a.scale = float(scale) if scale else 0.0
     a.dtype = _dtype_code(q)
     a.heavy_rows = int(heavy_rows)
+    a.kernel_select = int(kernel_select)
+    ran = ctypes.c_int32(0)
+    a.kernels_ran = ctypes.pointer(ran)
     lib = _lib.load()
     nbytes = int(lib.vb_attn_bwd_workspace_size(ctypes.byref(a)))
     ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
     a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
     check(lib.vb_attn_bwd(ctypes.byref(a), _stream(dev)), "vb_attn_bwd")
+    if kernels_ran is not None:
+        kernels_ran.append(ran.value)
     return dq, dk, dv
 
 
@@ -342,10 +378,11 @@ def mask_predict(q, k, q_off=None, k_off=None, *, rows=None, energy_threshold=0.
                              rows_kept=rows_kept)
     except Exception as e:
         # the claimed draws go back to the generator only when nothing was launched: a Python-side
-        # validation error, or the library refusing the call (VB_ERR_INVALID / _UNSUPPORTED, raised
-        # before any launch). After a VB_ERR_LAUNCH the sampling launch may already have consumed
-        # them, and rewinding would make the next torch.rand repeat those Philox values.
-        launched = isinstance(e, _lib.VBladeError) and e.code not in (_lib.VB_ERR_INVALID,
+        # error (validation, or a host-side VBladeError such as the library failing to load, code
+        # None), or the library refusing the call (VB_ERR_INVALID / _UNSUPPORTED, returned before
+        # any launch). After a VB_ERR_LAUNCH the sampling launch may already have consumed them, and
+        # rewinding would make the next torch.rand repeat those Philox values.
+        launched = isinstance(e, _lib.VBladeError) and e.code not in (None, _lib.VB_ERR_INVALID,
                                                                       _lib.VB_ERR_UNSUPPORTED)
         if philox is not None and not launched:
             release_rand_draws(q.device, philox)
@@ -357,10 +394,13 @@ def _mask_predict(q, k, q_off, k_off, *, rows, energy_threshold, min_keep, max_k
     if k.shape != q.shape:
         raise ValueError(f"mask_predict: k and v must have q's shape {tuple(q.shape)}, "
                          f"got k {tuple(k.shape)}")
-    dev = _require_gpu(q, k, q_off, k_off, rows)
+    dev = _require_gpu(q, k, q_off, k_off, rows, rows_kept)
     q, k = _aligned_bhld(q), _aligned_bhld(k)
     B, H, L, D = q.shape
     nb = (L + BLOCK - 1) // BLOCK
+    if rows_kept is not None and (level is not None or not want_mask):
+        raise ValueError("mask_predict: rows_kept is written by the energy rule only (not with level= "
+                         "or want_mask=False)")
     po = torch.empty(B, H, nb, nb, device=dev, dtype=q.dtype)
     mask = torch.empty(B, H, nb, nb, device=dev, dtype=torch.uint8) if want_mask else None
     if rand is not None and philox is not None:
@@ -427,6 +467,7 @@ def _mask_predict(q, k, q_off, k_off, *, rows, energy_threshold, min_keep, max_k
     if rows_kept is not None:
         if rows_kept.dtype != torch.int32 or rows_kept.numel() != B * H * nb or not rows_kept.is_contiguous():
             raise ValueError("mask_predict: rows_kept must be contiguous int32 [B,H,nb]")
+        _check_dev("mask_predict: rows_kept", rows_kept, dev)
         a.mask_rows_kept = rows_kept.data_ptr()
     check(lib.vb_mask_predict(ctypes.byref(a), _stream(dev)), "vb_mask_predict")
     return po, mask
@@ -651,7 +692,7 @@ def level_mask(po, ratios=None):
 
 
 def ml_attention_fwd(q, kpyr, vpyr, level_mask_u8, *, q_rows=None, scale=None, ref_tail=True,
-                     want_lse=False, heavy_rows=2, out=None):
+                     want_lse=False, heavy_rows=2, out=None, persistent: bool = False):
     """vb_ml_attn_fwd: multi-level attention of q [B,H,L,D] over the KV pyramids. Returns out
     (rows through q_rows) and, if want_lse, the fp32 natural-log LSE [B,H,L] (reordered rows)."""
     dev = _require_gpu(q, kpyr, vpyr, level_mask_u8, q_rows)
@@ -681,15 +722,18 @@ def ml_attention_fwd(q, kpyr, vpyr, level_mask_u8, *, q_rows=None, scale=None, r
     a.ref_tail = 1 if ref_tail else 0
     a.dtype = _dtype_code(q)
     a.heavy_rows = int(heavy_rows)
+    if persistent:
+        a.work_queue = work_queue(dev).data_ptr()
     check(_lib.load().vb_ml_attn_fwd(ctypes.byref(a), _stream(dev)), "vb_ml_attn_fwd")
     return (out, lse) if want_lse else out
 
 
 def ml_attention_bwd(dout, q, kpyr, vpyr, level_mask_u8, out, lse, *, rows=None, scale=None,
-                     ref_tail=True, heavy_rows=2):
+                     ref_tail=True, heavy_rows=2, kernel_select: int = 0, kernels_ran: Optional[list] = None):
     """vb_ml_attn_bwd: gradients of the multi-level attention. q/out/dout [B,H,L,D] (rows through
     ``rows``), pyramids and mask as the forward; lse as ml_attention_fwd(want_lse=True) wrote it.
-    Returns (dq, dk, dv) [B,H,L,D] in q's dtype (dk/dv at the caller's rows)."""
+    Returns (dq, dk, dv) [B,H,L,D] in q's dtype (dk/dv at the caller's rows). ``kernel_select`` /
+    ``kernels_ran`` as attention_bwd (VB_BWD_SEL_DQ_RING4 is refused here)."""
     dev = _require_gpu(dout, q, kpyr, vpyr, level_mask_u8, out, lse, rows)
     q, out, dout = _aligned_bhld(q), _aligned_bhld(out), _aligned_bhld(dout)
     B, H, L, D = q.shape
@@ -712,11 +756,16 @@ def ml_attention_bwd(dout, q, kpyr, vpyr, level_mask_u8, out, lse, *, rows=None,
     a.ref_tail = 1 if ref_tail else 0
     a.dtype = _dtype_code(q)
     a.heavy_rows = int(heavy_rows)
+    a.kernel_select = int(kernel_select)
+    ran = ctypes.c_int32(0)
+    a.kernels_ran = ctypes.pointer(ran)
     lib = _lib.load()
     nbytes = int(lib.vb_ml_attn_bwd_workspace_size(ctypes.byref(a)))
     ws = torch.empty(max(nbytes, 16), device=dev, dtype=torch.uint8)
     a.workspace, a.workspace_bytes = ws.data_ptr(), nbytes
     check(lib.vb_ml_attn_bwd(ctypes.byref(a), _stream(dev)), "vb_ml_attn_bwd")
+    if kernels_ran is not None:
+        kernels_ran.append(ran.value)
     return dq, dk, dv
 
 
