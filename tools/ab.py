@@ -44,7 +44,8 @@ def load(tag):
     return lib
 
 
-ORDER = [True, 0, False, 0]   # longest-first order, order window, persistent launch, backward kernel_select
+ORDER = [True, 0, False, 0]   # longest-first order, order window, persistent attention launch,
+                             # backward kernel_select
 
 
 def select(tag, libs):

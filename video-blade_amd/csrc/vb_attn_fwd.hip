@@ -19,7 +19,6 @@
 //                                        the S^T accumulator registers (no LDS round trip)
 // Gilbert reorder: q/k/v rows are gathered through q_rows / kv_rows and O/LSE scattered through
 // q_rows, so the reference's index_select + cat + reverse (:141-161) cost no pass of their own.
-#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -75,28 +74,12 @@ constexpr int fwd_smem_bytes() {
   return ((D == 64) ? 3 : 2) * 2 * kKT * D * 2 + kMaxBlocks * 2 + 16 + (kKvRows ? 4 * 512 : 0);
 }
 
-// Persistent dispatch (vb_attn_args.work_queue): the launch is resident-sized and every workgroup
-// pulls work items from per-XCD queue heads. Item v (a "virtual blockIdx" in [0, total)) belongs to
-// queue v % 8, in increasing v: the same items, in the same per-XCD order, as one workgroup per item
-// dealt round-robin over the XCDs. A workgroup drains its own XCD's queue (w % 8 shares an XCD, like
-// blockIdx % 8 of the one-per-item grid), then takes the remaining items of the other queues, so no
-// XCD idles while another still has work. Heads are 128 bytes apart; wq[kWqDone] counts finished
-// workgroups and the last one to finish zeroes every word, so each launch finds the queue at zero
-// (the buffer is zero before its first use).
-constexpr int kWqStride = 32;
-constexpr int kWqDone = 8 * kWqStride;
-__device__ __forceinline__ int wq_fetch(int* wq, int home, int total) {
-#pragma unroll 1
-  for (int i = 0; i < 8; ++i) {
-    const int x = (home + i) & 7;
-    const int cnt = (total - x + 7) >> 3;   // items x, x + 8, x + 16, ...
-    if (cnt > 0) {
-      const int j = __hip_atomic_fetch_add(wq + x * kWqStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (j < cnt) return x + 8 * j;
-    }
-  }
-  return -1;
-}
+// Persistent dispatch (vb_attn_args.work_queue; vb_common.hpp): the launch is resident-sized and
+// every workgroup pulls work items from per-XCD queue heads. Item v (a "virtual blockIdx" in [0,
+// total)) belongs to queue v % 8, in increasing v: the same items, in the same per-XCD order, as one
+// workgroup per item dealt round-robin over the XCDs. A workgroup drains its own XCD's queue (w % 8
+// shares an XCD, like blockIdx % 8 of the one-per-item grid), then takes the remaining items of the
+// other queues, so no XCD idles while another still has work.
 
 // One work item: the (b, h, 128-row q-block) of virtual blockIdx `vblk`. With a work queue, lane 0
 // of wave 0 claims the workgroup's next item at the start of the item's last tile (`next`), so the
@@ -1031,12 +1014,7 @@ __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) at
     item = next_s;
     __syncthreads();   // next_s is read by every wave before lane 0 may overwrite it
   }
-  if (wq && threadIdx.x == 0) {
-    // the last workgroup to finish (all fetches of every workgroup have returned) re-zeroes the queue
-    const int done = __hip_atomic_fetch_add(wq + kWqDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == (int)gridDim.x - 1)
-      for (int x = 0; x <= 8; ++x) __hip_atomic_store(wq + x * kWqStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (wq && threadIdx.x == 0) wq_finish(wq);   // the last workgroup re-zeroes the queue
 }
 
 // Dispatch order of the attention kernel's phase 2 (longest-processing-time first, per XCD): the
@@ -1130,18 +1108,8 @@ static unsigned fwd_grid(FwdParams& p) {
   const unsigned items = (unsigned)(p.nbq * p.B * p.H);
   p.n_items = (int)items;
   if (!p.work_queue) return items;
-  static std::atomic<int> slots_by_dev[64];   // 0 = not queried yet
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  int slots = slots_by_dev[dev].load(std::memory_order_relaxed);
-  if (slots == 0) {
-    int cus = 0, per_cu = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, Kern, kThreads, 0) != hipSuccess) per_cu = 0;
-    slots = cus * per_cu > 8 ? cus * per_cu / 8 * 8 : 8;
-    slots_by_dev[dev].store(slots, std::memory_order_relaxed);
-  }
-  return (unsigned)slots < items ? (unsigned)slots : items;
+  const unsigned slots = (unsigned)resident_grid(reinterpret_cast<const void*>(Kern), kThreads, 0);
+  return slots < items ? slots : items;
 }
 
 template <auto Kern>

@@ -93,6 +93,39 @@ __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_ex
 constexpr int kPoolWgsDefault = VB_POOL_WGS_DEFAULT;
 unsigned pool_grid(int64_t work_items);   // vb_pool.hip
 
+// ---------------------------------------------------------------- persistent work queues (ABI 4)
+// The caller's int32[VB_WORK_QUEUE_INTS] queue: heads 0-7 per XCD (work item v is in queue v % 8),
+// word kWqDone the finished workgroups. Words are 128 bytes apart. The last workgroup to finish a
+// launch zeroes every word (wq_finish), so each launch finds the queue at zero.
+constexpr int kWqStride = 32;
+constexpr int kWqDone = 8 * kWqStride;
+static_assert(kWqDone < VB_WORK_QUEUE_INTS, "work queue words");
+__device__ __forceinline__ int wq_pop(int* wq, int word) {
+  return __hip_atomic_fetch_add(wq + word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// next item of a per-XCD queue set over `total` items: the home XCD's queue first, then the others'
+__device__ __forceinline__ int wq_fetch(int* wq, int home, int total) {
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    const int x = (home + i) & 7;
+    const int cnt = (total - x + 7) >> 3;   // items x, x + 8, x + 16, ...
+    if (cnt > 0) {
+      const int j = wq_pop(wq, x * kWqStride);
+      if (j < cnt) return x + 8 * j;
+    }
+  }
+  return -1;
+}
+// called once per workgroup by one thread, after its last (failed) fetch has returned
+__device__ __forceinline__ void wq_finish(int* wq) {
+  const int done = wq_pop(wq, kWqDone);
+  if (done == (int)gridDim.x - 1)
+    for (int x = 0; x <= kWqDone / kWqStride; ++x)
+      __hip_atomic_store(wq + x * kWqStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// resident workgroups of `kernel` at `smem` bytes of dynamic LDS on the current device (host; no sync)
+int resident_grid(const void* kernel, int threads, size_t smem);
+
 // ---------------------------------------------------------------- host error plumbing
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);

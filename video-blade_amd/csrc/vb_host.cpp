@@ -5,7 +5,10 @@
 // cogvideox/train/special_attentions_local/utils/gilbert3d.py:6-167 and the coordinate->index map
 // of GilbertRearranger (TrainRelated/cogvideo_blocksparseattn.py:119-140).
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "vb_common.hpp"
@@ -27,6 +30,29 @@ int check_launch(const char* what) {
     return fail(VB_ERR_LAUNCH, std::string(what) + ": " + hipGetErrorString(e));
   }
   return VB_OK;
+}
+
+// Persistent launches: the occupancy of `kernel` at `smem` bytes of dynamic LDS times the device's
+// CUs, rounded down to a multiple of 8 (every XCD the same number of workgroups). Host queries only,
+// cached per (kernel, device, LDS size).
+int resident_grid(const void* kernel, int threads, size_t smem) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, size_t>, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const auto key = std::make_tuple(kernel, dev, smem);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, smem) != hipSuccess) per_cu = 0;
+  const int slots = cus * per_cu >= 8 ? cus * per_cu / 8 * 8 : 8;
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = slots;
+  return slots;
 }
 
 namespace {
