@@ -236,7 +236,7 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
   if (p.q_rows) qrow = p.q_rows[qrow];
   const uint8_t* qbase = reinterpret_cast<const uint8_t*>(p.q) + 2 * (b * p.qs[0] + h * p.qs[1] + qrow0 * p.qs[2]);
   typename T::vec8 qf[KS];
-  {
+  auto load_q = [&]() __attribute__((always_inline)) {
     const uint8_t* qp = qbase + (int64_t)qrow * 2 * p.qs[2];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
@@ -253,8 +253,19 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
     // on the global loads, so hipcc's waitcnt pass does not count them against the DMA ring.
 #pragma unroll
     for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]));
+  };
+  // kQLate: the Q fragment is loaded after the ring's first DMAs are issued (below), so its round
+  // trip and theirs overlap; only the q_rows entry (issued above) and the mask row precede the
+  // barrier. Otherwise Q is loaded first and retired before the DMA ring starts.
+  constexpr bool kQLate = D == 64 ? VB_FWD_QLATE64 : (kLazy && !kKvRows) ? VB_FWD_QLATE128_LAZY : VB_FWD_QLATE128;
+  if constexpr (kQLate) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave 0's list writes
+    __builtin_amdgcn_s_barrier();                           // kept-block list visible
+    asm volatile("" ::: "memory");
+  } else {
+    load_q();
+    __syncthreads();
   }
-  __syncthreads();   // kept-block list visible; Q loads retired before the DMA ring starts
   const int nkept = __builtin_amdgcn_readfirstlane(*list_n);
   // main tiles: two 64-key halves per kept block, minus an empty second half of the last block
   int ntm = 2 * nkept;
@@ -882,6 +893,7 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
     }
     next_blk = any_list_at(kBufs - 1);
   }
+  if constexpr (kQLate) load_q();   // its wait (vmcnt 0) also lands the ring's first tiles
   // The loop body is instantiated once per ring slot (compile-time U), so every LDS address is a
   // loop-invariant lane base + immediate offset: no address VALU inside the loop.
   auto body = [&](int t, auto U) __attribute__((always_inline)) {

@@ -63,6 +63,19 @@ struct FwdParams {
 #ifndef VB_FWD_PRIO128
 #define VB_FWD_PRIO128 3   // measured (Wan, 2 waves per SIMD): 3 +4.1/+4.5 %, 1 +2.5/+5.6 %, 7 +4.2 %, 2 -2.6 %, 4 +0.0 %
 #endif
+// the Q fragment loaded after the ring's first DMAs (their round trips overlap), per launch form.
+// Measured (tools/ab.py, r06, profiles/r06_qlate_ab.log): D=64 attention 1.044-1.048x, its LSE launch
+// 1.058x; D=128 LSE launch 1.047-1.049x, the inference launch on gathered K/V (Wan's module path)
+// 1.001-1.003x per call, on Gilbert copies 0.98x (kept off there)
+#ifndef VB_FWD_QLATE64
+#define VB_FWD_QLATE64 1
+#endif
+#ifndef VB_FWD_QLATE128
+#define VB_FWD_QLATE128 1
+#endif
+#ifndef VB_FWD_QLATE128_LAZY
+#define VB_FWD_QLATE128_LAZY 0   // D=128 inference launch on contiguous (copied) K/V
+#endif
 #ifndef VB_FWD_WAVES_D64
 #define VB_FWD_WAVES_D64 3  // waves per SIMD the D=64 kernel is register-budgeted for
 #endif
