@@ -16,13 +16,16 @@ HIPCC = "/opt/rocm/bin/hipcc"
 
 # the product launches: <D, BF16, pooled, no kv_rows, not multi-level, kCBias> and the LSE launch
 KERNELS = [
-    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb1EEEvNS_9FwdParamsE",
-    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb1EEEvNS_9FwdParamsE",
-    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb0EEEvNS_9FwdParamsE",
-    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb0EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb1ELb0EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb1ELb0EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb0ELb0EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb0ELb0ELb0ELb0EEEvNS_9FwdParamsE",
     # the module's path: K/V rows gathered through the Gilbert index
-    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb1ELb0ELb1EEEvNS_9FwdParamsE",
-    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb1ELb0ELb1EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb1ELb0ELb1ELb0EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi128ENS_4BF16ELb1ELb1ELb0ELb1ELb0EEEvNS_9FwdParamsE",
+    # the persistent (work-queue) CogVideoX launches
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb1ELb1EEEvNS_9FwdParamsE",
+    "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb1ELb0ELb1ELb1EEEvNS_9FwdParamsE",
 ]
 
 
@@ -59,6 +62,35 @@ def test_no_scratch_reload_in_dma_issue_blocks(fwd_asm, name):
     bad = [b[0] for b in _blocks(fwd_asm, name)
            if any("offen lds" in l for l in b) and any("scratch_load" in l for l in b)]
     assert not bad, f"{name}: spill reloads in LDS-DMA issue blocks {bad[:4]}"
+
+
+def _hot_loop_vmcnt_waits(asm, name):
+    """s_waitcnt vmcnt instructions of the loop that holds the kernel's MFMAs (the tile loop)."""
+    i = asm.index(name + ":")
+    j = asm.index(".Lfunc_end", i)
+    loops, cur = {}, None
+    for line in asm[i:j].split("\n"):
+        if re.match(r"^(\.LBB\S+:|; %bb\.\d+:)", line):
+            m = re.search(r"Header=(\S+)", line)
+            cur = m.group(1) if m else ("self:" + line.split()[0] if "Loop Header" in line else "")
+            loops.setdefault(cur, [])
+        elif cur is not None:
+            loops.setdefault(cur, []).append(line.strip())
+    hot = max(loops.values(), key=lambda ls: sum("v_mfma" in x for x in ls))
+    return sum(x.startswith("s_waitcnt") and "vmcnt" in x for x in hot)
+
+
+@pytest.mark.parametrize("base", ["_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb1E",
+                                  "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb1ELb0ELb1E"])
+def test_persistent_tile_loop_waits_like_the_per_item_loop(fwd_asm, base):
+    """Round 6: wrapped in the persistent item loop, the tile loop once compiled with extra
+    `s_waitcnt vmcnt(0)` (hipcc's waitcnt pass guarding LDS reads against LDS-DMA it could no longer
+    separate, and the work-queue claim inside the loop): each drains the DMA ring, 6-7 % of the
+    kernel. The persistent launches the module uses must wait exactly as often per round as the
+    one-workgroup-per-q-block kernel."""
+    per_item = _hot_loop_vmcnt_waits(fwd_asm, base + "Lb0EEEvNS_9FwdParamsE")
+    persistent = _hot_loop_vmcnt_waits(fwd_asm, base + "Lb1EEEvNS_9FwdParamsE")
+    assert persistent == per_item, (persistent, per_item)
 
 
 def test_makefile_falls_back_when_the_scheduler_option_is_gone():

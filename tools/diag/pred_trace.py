@@ -4,7 +4,9 @@ tools/build_variant.sh ptrace) or of the attention kernel's (what = attn; VB_EXT
 tools/build_variant.sh atrace): start and per-wave end times (s_memrealtime, 10 ns), CU and XCD of
 every workgroup, and the shader clock over it. Prints how long the workgroups live, when they start,
 and how many are resident per CU over the launch (slot utilisation, the tail).
-usage: python tools/diag/pred_trace.py [cog|wan] [pred|call|attn] [TAG]"""
+usage: python tools/diag/pred_trace.py [cog|wan] [pred|call|attn] [TAG]
+(attn: TRACE_PERSIST=0 traces the one-workgroup-per-q-block launch; with the persistent launch every
+work item is one record, and the gaps between a workgroup's items count as idle slot time)"""
 import ctypes
 import os
 import sys
@@ -32,6 +34,7 @@ _lib._lib = lib
 dev = torch.device("cuda")
 H, D = (48, 64) if variant == "cog" else (12, 128)
 m = vblade.AdaptiveBlockSparseAttn(variant, log_every=0)
+m.persistent = os.environ.get("TRACE_PERSIST", "1") != "0"   # the attention launch's dispatch form
 L = m.gilbert_rearranger.seq_len
 q, k, v = realistic_qkv(H, L, D, 0, dev)
 qo = vblade.draw_sample_offsets(1, H, dev)

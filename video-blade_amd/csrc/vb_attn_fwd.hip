@@ -82,10 +82,10 @@ constexpr int fwd_smem_bytes() {
 // other queues, so no XCD idles while another still has work.
 
 // One work item: the (b, h, 128-row q-block) of virtual blockIdx `vblk`. With a work queue, lane 0
-// of wave 0 claims the workgroup's next item at the start of the item's last tile (`next`), so the
-// claim's round trip overlaps that tile and the epilogue.
-template <int D, class T, bool kPool, bool kKvRows, bool kML, bool kCBias>
-__device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk, uint8_t* smem, int& next) {
+// of wave 0 claims the workgroup's next item after the tile loop (`next`), so the claim's round
+// trip overlaps the epilogue.
+template <int D, class T, bool kPool, bool kKvRows, bool kML, bool kCBias, bool kWQ>
+__device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk, int& next) {
   constexpr int KS = D / 16;                   // k-steps of the QK^T product
   constexpr int DT = D / 32;                   // 32-wide d tiles of the output
   constexpr bool kSplitPV = VB_FWD_SPLIT_PV && D == 64;   // measured: +0.8 % at D=64, -1.4 % at D=128
@@ -108,6 +108,10 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
   constexpr int kRowsPerInst = 1024 / kRowB;   // rows one 1-KiB LDS-DMA wave-instruction fills
   constexpr int kInstPerMat = kMatBytes / 1024;
   constexpr int kInstPerWave = 2 * kInstPerMat / 4;
+  // declared here, not passed in from the kernel: hipcc's waitcnt pass then still sees which LDS
+  // bytes each LDS-DMA writes and each read reads (through a pointer parameter it puts a vmcnt wait,
+  // draining the ring, in front of every LDS read of the loop)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[fwd_smem_bytes<D, kKvRows>()];
   static_assert(fwd_smem_bytes<D, kKvRows>() == kBufs * kBufBytes + kMaxBlocks * 2 + 16 + (kKvRows ? 4 * 512 : 0), "LDS layout");
   static_assert(!(kML && (kPool || kKvRows)), "multi-level mode reads the KV pyramids only");
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
@@ -115,8 +119,15 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
 
   // The thread id is laundered per item: otherwise the persistent loop hoists every lane-derived
   // address (DMA chunks, LDS fragment bases) out of the item loop and spills them across it.
+  // Persistent launches (kWQ) launder the thread id per item: otherwise the item loop hoists the
+  // lane-derived addresses (DMA chunks, LDS fragment bases) out of it and spills them across it.
+  // The mask keeps its range known (0..255), so hipcc's waitcnt pass still separates a ring slot's
+  // LDS-DMA from the reads of another slot.
   int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
+  if constexpr (kWQ) {
+    asm volatile("" : "+v"(tid));
+    tid &= kThreads - 1;
+  }
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -947,14 +958,20 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
     VB_ACC(2, st3 - st2);
   };
   for (int t0 = 0; t0 < ntiles; t0 += kBufs) {
-    if (p.work_queue && t0 + kBufs >= ntiles && tid == 0)   // the last ring round: claim the next item
-      next = wq_fetch(p.work_queue, blockIdx.x & 7, p.n_items);
     body(t0, std::integral_constant<int, 0>{});
     if (t0 + 1 < ntiles) body(t0 + 1, std::integral_constant<int, 1>{});
     if constexpr (kBufs > 2)
       if (t0 + 2 < ntiles) body(t0 + 2, std::integral_constant<int, 2>{});
   }
-  if constexpr (kKvRows) VB_WAIT_VMCNT(0);   // the stages issued past the last tile land before exit
+  // the stages issued past the last tile land before exit; persistent launches always wait here (a
+  // no-op at run time: every tile has landed): across the item loop's back edge hipcc's waitcnt pass
+  // would otherwise count LDS-DMA as possibly in flight and wait (drain the ring) before the next
+  // item's LDS reads
+  if constexpr (kKvRows || kWQ) VB_WAIT_VMCNT(0);
+  // The next item is claimed here, after the tile loop and before the epilogue's arithmetic and
+  // stores, so its round trip overlaps them. Not inside the loop: the claim's wait for its own
+  // result (and the waits hipcc then places after the branch) would drain the DMA ring every round.
+  if (kWQ && tid == 0) next = wq_fetch(p.work_queue, blockIdx.x & 7, p.n_items);
 #if VB_DIAG
   if (lane == 0) {
     for (int i = 0; i < 5; ++i) atomicAdd(&g_vb_stamp[i], acc_st[i]);
@@ -1005,28 +1022,29 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
   VB_ATRACE_END();
 }
 
-template <int D, class T, bool kPool, bool kKvRows, bool kML = false, bool kCBias = false>
+template <int D, class T, bool kPool, bool kKvRows, bool kML = false, bool kCBias = false, bool kPersist = false>
 __global__ void __launch_bounds__(kThreads, (D == 64 ? VB_FWD_WAVES_D64 : 2)) attn_fwd_kernel(const FwdParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[fwd_smem_bytes<D, kKvRows>()];
-  __shared__ int next_s;
-  int* const wq = p.work_queue;
-  int item = blockIdx.x;
-  if (wq) {   // persistent: the first item from the queue too (the grid is resident-sized)
+  if constexpr (!kPersist) {   // one workgroup per item
+    int next;
+    attn_fwd_item<D, T, kPool, kKvRows, kML, kCBias, false>(p, blockIdx.x, next);
+  } else {
+    // persistent: a resident-sized grid, every item (the first one too) from the work queue
+    __shared__ int next_s;
+    int* const wq = p.work_queue;
     if (threadIdx.x == 0) next_s = wq_fetch(wq, blockIdx.x & 7, p.n_items);
     __syncthreads();
-    item = next_s;
+    int item = next_s;
+    while (item >= 0) {
+      int next = -2;   // -2: not claimed during the item (it returned before its tile loop)
+      attn_fwd_item<D, T, kPool, kKvRows, kML, kCBias, true>(p, item, next);
+      // every wave is done with this item's LDS (ring, list) before the next item's prologue writes it
+      if (threadIdx.x == 0) next_s = next == -2 ? wq_fetch(wq, blockIdx.x & 7, p.n_items) : next;
+      __syncthreads();
+      item = next_s;
+      __syncthreads();   // next_s is read by every wave before lane 0 may overwrite it
+    }
+    if (threadIdx.x == 0) wq_finish(wq);   // the last workgroup re-zeroes the queue
   }
-  while (item >= 0) {
-    int next = -2;   // -2: not claimed during the item (it had no tile)
-    attn_fwd_item<D, T, kPool, kKvRows, kML, kCBias>(p, item, smem, next);
-    if (!wq) break;
-    // every wave is done with this item's LDS (ring, list) before the next item's prologue writes it
-    if (threadIdx.x == 0) next_s = next == -2 ? wq_fetch(wq, blockIdx.x & 7, p.n_items) : next;
-    __syncthreads();
-    item = next_s;
-    __syncthreads();   // next_s is read by every wave before lane 0 may overwrite it
-  }
-  if (wq && threadIdx.x == 0) wq_finish(wq);   // the last workgroup re-zeroes the queue
 }
 
 // Dispatch order of the attention kernel's phase 2 (longest-processing-time first, per XCD): the
@@ -1115,19 +1133,18 @@ __global__ void __launch_bounds__(1024) attn_order_kernel(const FwdParams p, int
 // Grid of one launch: one workgroup per item, or (work queue) as many as are resident at once —
 // the occupancy of this instantiation times the device's CUs (host queries, cached per kernel and
 // device; no device synchronisation), a multiple of 8 so every XCD gets the same number.
-template <auto Kern>
-static unsigned fwd_grid(FwdParams& p) {
+// Grid of one launch: one workgroup per item, or (persistent instantiation, with a work queue) as
+// many as are resident at once (resident_grid: occupancy x CUs, a multiple of 8).
+template <auto Kern, auto KernP>
+static int launch_one(FwdParams p, hipStream_t stream, const char* what) {
   const unsigned items = (unsigned)(p.nbq * p.B * p.H);
   p.n_items = (int)items;
-  if (!p.work_queue) return items;
-  const unsigned slots = (unsigned)resident_grid(reinterpret_cast<const void*>(Kern), kThreads, 0);
-  return slots < items ? slots : items;
-}
-
-template <auto Kern>
-static int launch_one(FwdParams p, hipStream_t stream, const char* what) {
-  const unsigned grid = fwd_grid<Kern>(p);
-  hipLaunchKernelGGL(Kern, dim3(grid), dim3(kThreads), 0, stream, p);
+  if (p.work_queue) {
+    const unsigned slots = (unsigned)resident_grid(reinterpret_cast<const void*>(KernP), kThreads, 0);
+    hipLaunchKernelGGL(KernP, dim3(slots < items ? slots : items), dim3(kThreads), 0, stream, p);
+  } else {
+    hipLaunchKernelGGL(Kern, dim3(items), dim3(kThreads), 0, stream, p);
+  }
   return check_launch(what);
 }
 
@@ -1136,14 +1153,14 @@ static int launch_fwd(const FwdParams& p, bool pool, hipStream_t stream) {
   const bool rows = p.kv_rows != nullptr;
   const bool cbias = VB_FWD_CBIAS && p.lse == nullptr;
   const char* w = "attn_fwd_kernel";
-  if (cbias && pool && rows) return launch_one<attn_fwd_kernel<D, T, true, true, false, true>>(p, stream, w);
-  if (cbias && rows) return launch_one<attn_fwd_kernel<D, T, false, true, false, true>>(p, stream, w);
-  if (cbias && pool) return launch_one<attn_fwd_kernel<D, T, true, false, false, true>>(p, stream, w);
-  if (cbias) return launch_one<attn_fwd_kernel<D, T, false, false, false, true>>(p, stream, w);
-  if (pool && rows) return launch_one<attn_fwd_kernel<D, T, true, true>>(p, stream, w);
-  if (pool) return launch_one<attn_fwd_kernel<D, T, true, false>>(p, stream, w);
-  if (rows) return launch_one<attn_fwd_kernel<D, T, false, true>>(p, stream, w);
-  return launch_one<attn_fwd_kernel<D, T, false, false>>(p, stream, w);
+  if (cbias && pool && rows) return launch_one<attn_fwd_kernel<D, T, true, true, false, true, false>, attn_fwd_kernel<D, T, true, true, false, true, true>>(p, stream, w);
+  if (cbias && rows) return launch_one<attn_fwd_kernel<D, T, false, true, false, true, false>, attn_fwd_kernel<D, T, false, true, false, true, true>>(p, stream, w);
+  if (cbias && pool) return launch_one<attn_fwd_kernel<D, T, true, false, false, true, false>, attn_fwd_kernel<D, T, true, false, false, true, true>>(p, stream, w);
+  if (cbias) return launch_one<attn_fwd_kernel<D, T, false, false, false, true, false>, attn_fwd_kernel<D, T, false, false, false, true, true>>(p, stream, w);
+  if (pool && rows) return launch_one<attn_fwd_kernel<D, T, true, true, false, false, false>, attn_fwd_kernel<D, T, true, true, false, false, true>>(p, stream, w);
+  if (pool) return launch_one<attn_fwd_kernel<D, T, true, false, false, false, false>, attn_fwd_kernel<D, T, true, false, false, false, true>>(p, stream, w);
+  if (rows) return launch_one<attn_fwd_kernel<D, T, false, true, false, false, false>, attn_fwd_kernel<D, T, false, true, false, false, true>>(p, stream, w);
+  return launch_one<attn_fwd_kernel<D, T, false, false, false, false, false>, attn_fwd_kernel<D, T, false, false, false, false, true>>(p, stream, w);
 }
 
 static int dispatch_fwd(const FwdParams& p, int D, int dtype, bool pool, hipStream_t stream) {
@@ -1290,16 +1307,16 @@ extern "C" int vb_ml_attn_fwd(const vb_ml_attn_args* a, void* stream) {
   const bool cb = VB_FWD_CBIAS && p.lse == nullptr;   // inference launches (see kCBias)
   const char* w = "attn_fwd_kernel (multi-level)";
   if (a->dtype == VB_DTYPE_BF16) {
-    if (a->D == 64 && cb) return launch_one<attn_fwd_kernel<64, BF16, false, false, true, true>>(p, st, w);
-    if (a->D == 64) return launch_one<attn_fwd_kernel<64, BF16, false, false, true>>(p, st, w);
-    if (cb) return launch_one<attn_fwd_kernel<128, BF16, false, false, true, true>>(p, st, w);
-    return launch_one<attn_fwd_kernel<128, BF16, false, false, true>>(p, st, w);
+    if (a->D == 64 && cb) return launch_one<attn_fwd_kernel<64, BF16, false, false, true, true, false>, attn_fwd_kernel<64, BF16, false, false, true, true, true>>(p, st, w);
+    if (a->D == 64) return launch_one<attn_fwd_kernel<64, BF16, false, false, true, false, false>, attn_fwd_kernel<64, BF16, false, false, true, false, true>>(p, st, w);
+    if (cb) return launch_one<attn_fwd_kernel<128, BF16, false, false, true, true, false>, attn_fwd_kernel<128, BF16, false, false, true, true, true>>(p, st, w);
+    return launch_one<attn_fwd_kernel<128, BF16, false, false, true, false, false>, attn_fwd_kernel<128, BF16, false, false, true, false, true>>(p, st, w);
   }
   if (a->dtype == VB_DTYPE_F16) {
-    if (a->D == 64 && cb) return launch_one<attn_fwd_kernel<64, F16, false, false, true, true>>(p, st, w);
-    if (a->D == 64) return launch_one<attn_fwd_kernel<64, F16, false, false, true>>(p, st, w);
-    if (cb) return launch_one<attn_fwd_kernel<128, F16, false, false, true, true>>(p, st, w);
-    return launch_one<attn_fwd_kernel<128, F16, false, false, true>>(p, st, w);
+    if (a->D == 64 && cb) return launch_one<attn_fwd_kernel<64, F16, false, false, true, true, false>, attn_fwd_kernel<64, F16, false, false, true, true, true>>(p, st, w);
+    if (a->D == 64) return launch_one<attn_fwd_kernel<64, F16, false, false, true, false, false>, attn_fwd_kernel<64, F16, false, false, true, false, true>>(p, st, w);
+    if (cb) return launch_one<attn_fwd_kernel<128, F16, false, false, true, true, false>, attn_fwd_kernel<128, F16, false, false, true, true, true>>(p, st, w);
+    return launch_one<attn_fwd_kernel<128, F16, false, false, true, false, false>, attn_fwd_kernel<128, F16, false, false, true, false, true>>(p, st, w);
   }
   return fail(VB_ERR_INVALID, "vb_ml_attn_fwd: unknown dtype");
 }

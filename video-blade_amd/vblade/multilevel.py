@@ -132,7 +132,7 @@ class AdaptiveBlockSparseAttnTrain(nn.Module):
     include/vblade.h, vb_ml_attn_fwd)."""
 
     def __init__(self, *, mask_ratios=None, ref_tail: bool = True, log_every: int = 600,
-                 overlap: bool = True, persistent: bool = True, **overrides):
+                 overlap: bool = True, persistent: bool = False, **overrides):
         """overlap: run the KV pyramid pass inside the predictor's launch (True) or as its own
         launch after it. persistent: the attention launch is resident-sized and pulls q-blocks
         from per-XCD work queues (scheduling only; see attention.PERSISTENT_DEFAULT)."""
