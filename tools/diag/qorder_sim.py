@@ -129,11 +129,41 @@ def main():
                 left.discard(int(best))
             og += [(h, i) for i in cur]
         orders[f"greedy{win}"] = og
+    # round 6: the order the kernel runs since ABI 3 (attn_order_kernel: longest first inside each
+    # XCD range), the same with ties broken by head and first kept off-diagonal block, and the
+    # greedy chain restricted to what a per-XCD queue can realise (inside each XCD's range, from its
+    # longest q-block, heads mixed as the range mixes them)
+    cnt = mask.sum(-1)
+    def first_kept(h, i):
+        js = [j for j in np.nonzero(mask[h, i])[0] if j != i]
+        return js[0] if js else i
+    lf, lfk, gx = [], [], []
+    m = mask.astype(np.int32)
+    for a, b in xcd_ranges(H, nb):
+        r = orders["default"][a:b]
+        lf += sorted(r, key=lambda x: -cnt[x])
+        lfk += sorted(r, key=lambda x: (-cnt[x], x[0], first_kept(*x)))
+        V = np.zeros((len(r), H * nb), np.int32)
+        for k, (h, i) in enumerate(r):
+            V[k, h * nb:(h + 1) * nb] = m[h, i]
+        left = set(range(len(r)))
+        cur = [max(left, key=lambda k: cnt[r[k]])]
+        left.discard(cur[0])
+        while left:
+            ref = V[cur[-8:]].sum(0)
+            cand = np.array(sorted(left))
+            best = int(cand[np.argmax(V[cand] @ ref)])
+            cur.append(best)
+            left.discard(best)
+        gx += [r[k] for k in cur]
+    orders["longest1st"] = lf
+    orders["lf+head+fk"] = lfk
+    orders["greedy8/xcd"] = gx
     for name, o in orders.items():
         tot = 0
         for a, b in xcd_ranges(H, nb):
             tot += simulate(o[a:b], mask, D, L, cfg.sample_gap)
-        print(f"  {name:9s} fetched {tot / 1e6:8.1f} MB = {tot / comp:5.2f}x compulsory K/V")
+        print(f"  {name:11s} fetched {tot / 1e6:8.1f} MB = {tot / comp:5.2f}x compulsory K/V")
 
 
 if __name__ == "__main__":

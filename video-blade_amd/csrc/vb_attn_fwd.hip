@@ -117,8 +117,6 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + kBufs * kBufBytes);
   int* list_n = reinterpret_cast<int*>(smem + kBufs * kBufBytes + kMaxBlocks * 2);
 
-  // The thread id is laundered per item: otherwise the persistent loop hoists every lane-derived
-  // address (DMA chunks, LDS fragment bases) out of the item loop and spills them across it.
   // Persistent launches (kWQ) launder the thread id per item: otherwise the item loop hoists the
   // lane-derived addresses (DMA chunks, LDS fragment bases) out of it and spills them across it.
   // The mask keeps its range known (0..255), so hipcc's waitcnt pass still separates a ring slot's
