@@ -675,6 +675,16 @@ def test_dispatch_order_small_shapes_batches_and_windows(B, H, L, D, heavy, wind
                             order_window=window, q_order_out=qo)
     got2 = ops.attention_fwd(q, k, v, block_mask=mask, heavy_rows=heavy, order=True, order_window=window)
     assert torch.equal(got, ref) and torch.equal(got2, ref)
+    # the persistent launch at the same shapes: fewer items than resident workgroups (most exit on
+    # their first claim), ragged last q-blocks, heavy rows beyond nbq; the queue is zero afterwards
+    for order in (False, True):
+        got3 = ops.attention_fwd(q, k, v, block_mask=mask, heavy_rows=heavy, order=order,
+                                 order_window=window, persistent=True)
+        assert torch.equal(got3, ref), order
+    o1, l1 = ops.attention_fwd(q, k, v, block_mask=mask, heavy_rows=heavy, need_lse=True)
+    o2, l2 = ops.attention_fwd(q, k, v, block_mask=mask, heavy_rows=heavy, need_lse=True, persistent=True)
+    assert torch.equal(o1, o2) and torch.equal(l1, l2)
+    assert int(ops.work_queue(q.device).abs().sum()) == 0
     qo, kc = qo.cpu(), kept.view(-1).cpu()
     rows_left = nb - min(heavy, nb)
     nwg = rows_left * B * H
