@@ -61,14 +61,15 @@ with torch.no_grad():
         mask = band.to(mask.dtype).expand_as(mask).contiguous()
         print(f"band mask: {kk} of {nb} blocks per row")
     kp, vp, k_r, v_r = ops.pool_kv(k, v, m.sample_gap, rows, reordered=True)
-    # the module's K/V source (gather_kv="auto": gathered rows at D=128, Gilbert copies at D=64), so
-    # the counters describe the same kernel variant that bench.py times
+    # the module's K/V source (gather_kv="auto": gathered rows at D=128, Gilbert copies at D=64),
+    # dispatch order and persistent launch, so the counters describe the kernel bench.py times
     gather = m._gather(D)
     k_src, v_src, kv_rows = (k, v, rows) if gather else (k_r, v_r, None)
     for _ in range(n):
         if what in ("attn", "all"):
             ops.attention_fwd(q, k_src, v_src, block_mask=mask, q_rows=rows, kv_rows=kv_rows, kp=kp,
-                              vp=vp, kp_log_bias=m._log_gap(q.dtype), heavy_rows=m.force_tail)
+                              vp=vp, kp_log_bias=m._log_gap(q.dtype), heavy_rows=m.force_tail,
+                              order=m.order, order_window=m.order_window, persistent=m.persistent)
         if what in ("pred", "all"):
             m.predict_mask(q, k, qo, ko)
     torch.cuda.synchronize()
