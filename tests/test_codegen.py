@@ -80,14 +80,19 @@ def _hot_loop_vmcnt_waits(asm, name):
     return sum(x.startswith("s_waitcnt") and "vmcnt" in x for x in hot)
 
 
-@pytest.mark.parametrize("base", ["_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb0ELb0ELb1E",
-                                  "_ZN2vb15attn_fwd_kernelILi64ENS_4BF16ELb1ELb1ELb0ELb1E"])
+@pytest.mark.parametrize("base", [f"_ZN2vb15attn_fwd_kernelILi{d}ENS_4BF16ELb{pool}ELb{kv}ELb{ml}ELb{cb}E"
+                                  for d in (64, 128) for cb in (0, 1)
+                                  for pool, kv, ml in ((1, 0, 0), (1, 1, 0), (0, 0, 1))])
 def test_persistent_tile_loop_waits_like_the_per_item_loop(fwd_asm, base):
     """Round 6: wrapped in the persistent item loop, the tile loop once compiled with extra
     `s_waitcnt vmcnt(0)` (hipcc's waitcnt pass guarding LDS reads against LDS-DMA it could no longer
     separate, and the work-queue claim inside the loop): each drains the DMA ring, 6-7 % of the
-    kernel. The persistent launches the module uses must wait exactly as often per round as the
-    one-workgroup-per-q-block kernel."""
+    kernel. The persistent launches must wait exactly as often per round as the
+    one-workgroup-per-q-block kernel: every launch form (D=64/128, contiguous or gathered K/V,
+    multi-level, with and without the LSE). At D=128 that needs the K/V LDS-DMA issued through an
+    address hipcc cannot trace to the LDS variable (`dma16_unscoped`): its waitcnt pass compares
+    LDS reads with ONE representative DMA per alias scope, and across the item loop that one
+    aliased the ring slot and the block list being read."""
     per_item = _hot_loop_vmcnt_waits(fwd_asm, base + "Lb0EEEvNS_9FwdParamsE")
     persistent = _hot_loop_vmcnt_waits(fwd_asm, base + "Lb1EEEvNS_9FwdParamsE")
     assert persistent == per_item, (persistent, per_item)

@@ -419,7 +419,8 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
     const int soffB = __builtin_amdgcn_readfirstlane(src.srcB * my_rowb);
 #pragma unroll
     for (int i = 0; i < kInstPerWave; ++i)
-      dma16(my_rsrc, dst + i * 1024, my_voff[i], (i * kRowsPerInst >= 16) ? soffB : soffA);
+      if constexpr (kWQ && VB_FWD_DMA_UNSCOPED) dma16_unscoped(my_rsrc, dst + i * 1024, my_voff[i], (i * kRowsPerInst >= 16) ? soffB : soffA);
+      else dma16(my_rsrc, dst + i * 1024, my_voff[i], (i * kRowsPerInst >= 16) ? soffB : soffA);
   };
   // Gathered K/V rows (kv_rows: reordered key -> caller row; the module's path on the caller's own
   // k/v). Per tile every wave DMAs the kv_rows entries of its own 32 rows into a 4-slot LDS ring
@@ -437,16 +438,25 @@ __device__ __forceinline__ void attn_fwd_item(const FwdParams& p, const int vblk
       const int kstart = __builtin_amdgcn_readfirstlane(blk_raw) * kQBlk + (t & 1) * kKT;
       voff = 4 * (kstart + min(gather_key, min(kKT, Lk - kstart) - 1));
     }
-    if (lane < 32)
+    if (lane < 32) {
+      uint8_t* dst = ibase + (t & 3) * 512;
+      if constexpr (kWQ && VB_FWD_DMA_UNSCOPED) {   // as dma16_unscoped
+        uint32_t a = __builtin_amdgcn_readfirstlane(
+            static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)dst)));
+        asm("" : "+s"(a));
+        dst = (uint8_t*)(__attribute__((address_space(3))) uint8_t*)(uintptr_t)a;
+      }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(rows_srd.base), (short)0, rows_srd.bytes, 0x00020000),
-          (__attribute__((address_space(3))) void*)(ibase + (t & 3) * 512), 4, voff, 0, 0, 0);
+          (__attribute__((address_space(3))) void*)dst, 4, voff, 0, 0, 0);
+    }
   };
   auto issue = [&](const TileSrc src, int slot, int t = 0) __attribute__((always_inline)) {
     uint8_t* dst = smem + slot * kBufBytes + my_mat * kMatBytes + (wave & 1) * kInstPerWave * 1024;
     // this wave's i-th 1 KiB piece of the tile
     auto piece = [&](int i, srd_t sd, int voff, int soff) __attribute__((always_inline)) {
-      dma16(sd, dst + i * 1024, voff, soff);
+      if constexpr (kWQ && VB_FWD_DMA_UNSCOPED) dma16_unscoped(sd, dst + i * 1024, voff, soff);
+      else dma16(sd, dst + i * 1024, voff, soff);
     };
     const bool pooled = kPool && src.pooled;
     if (kKvRows && !pooled) {

@@ -48,6 +48,9 @@ struct FwdParams {
 #ifndef VB_FWD_SPLIT_PV
 #define VB_FWD_SPLIT_PV 1   // D=64: P.V of the first 32 keys issued before the exp of the second 32
 #endif
+#ifndef VB_FWD_DMA_UNSCOPED
+#define VB_FWD_DMA_UNSCOPED 1   // persistent launches: K/V DMAs invisible to hipcc's LDS-DMA waits
+#endif
 #ifndef VB_FWD_CBIAS
 #define VB_FWD_CBIAS 1      // S accumulator seeded with (bias - m), Q pre-scaled: no per-score fma
 #endif

@@ -109,6 +109,18 @@ __device__ __forceinline__ void dma16(srd_t srd, uint8_t* lds, int voffset, int 
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(srd.base), (short)0, srd.bytes, 0x00020000),
       (__attribute__((address_space(3))) void*)lds, 16, voffset, soffset, 0, 0);
 }
+// dma16 with the LDS address passed through an empty asm (an SGPR value the optimizer cannot trace
+// to the LDS variable): the DMA's LDS store then carries no alias scope, and hipcc's waitcnt pass
+// puts no vmcnt wait of its own in front of LDS reads for it. For kernels that retire every DMA
+// with their own counted waits and barriers before reading its bytes.
+__device__ __forceinline__ void dma16_unscoped(srd_t srd, uint8_t* lds, int voffset, int soffset) {
+  uint32_t a = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds)));
+  asm("" : "+s"(a));
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(srd.base), (short)0, srd.bytes, 0x00020000),
+      (__attribute__((address_space(3))) void*)(uintptr_t)a, 16, voffset, soffset, 0, 0);
+}
 
 // 16-bit store through a buffer descriptor: lane address = base + voffset + soffset (no 64-bit
 // per-lane address arithmetic on the VALU)

@@ -47,8 +47,10 @@ VARIANT_DEFAULTS = {
 ORDER_DEFAULT = {"cog": False, "wan": True}
 
 # persistent attention launch (resident-sized grid, per-XCD work queues; ops.attention_fwd
-# persistent=True), per variant. The D=128 persistent kernel compiles with extra ring waits in its
-# tile loop, so Wan keeps one workgroup per q-block.
+# persistent=True), per variant. Measured (tools/ab.py, profiles/r06_persist_split_ab.log,
+# r06_persist_unscoped_ab.log): CogVideoX attention 1.005-1.009x; Wan's inference launch (gathered
+# K/V) 0.98x per call, so Wan keeps one workgroup per q-block (its LSE training launch runs
+# persistent: autograd.py).
 PERSISTENT_DEFAULT = {"cog": True, "wan": False}
 
 

@@ -59,8 +59,10 @@ class _AdaptiveSplitFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, mask, rows, gap, heavy_rows):
         kp, vp, k_r, v_r = ops.pool_kv(k, v, gap, rows, reordered=True)
+        # the persistent (work-queue) launch at D=128: Wan's LSE forward 1.024-1.030x, CogVideoX's
+        # 0.98x (profiles/r06_persist_unscoped_ab.log); bit-identical either way
         out1, lse1 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,
-                                       heavy_rows=heavy_rows)
+                                       heavy_rows=heavy_rows, persistent=q.shape[-1] == 128)
         out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
                                        need_lse=True)
         out, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
