@@ -340,3 +340,28 @@ def test_full_size_b5_training_batch_one_head():
     rq, rk, rv = O.adaptive_attention_bwd(q[:1], k[:1], v[:1], do[:1], cfg, fwd)
     for name, g, r in (("dq", qd.grad[:1], rq), ("dk", kd.grad[:1], rk), ("dv", vd.grad[:1], rv)):
         assert rel(g, r) <= TOL, (name, rel(g, r))
+
+
+def test_d128_backward_dq_side_stream_is_joined():
+    """Round 6: at D=128 the backward launches dQ on a library-owned side stream beside the dK/dV
+    chain (ForkScope, vb_attn_bwd.hip) and joins it back with an event before returning. Work on
+    the caller's stream right after the call must see the finished dQ: a reduction queued on the
+    caller's (non-default) stream without any synchronisation equals the one taken after a device
+    synchronize, over repeated calls, and the gradients are the same bits every time."""
+    B, H, L, D = 1, 4, 1000, 128
+    q, k, v, do = (_rand(B, H, L, D, seed=40 + s).to(DEV) for s in range(4))
+    nb = (L + 127) // 128
+    mask = O.block_mask_from_density(B, H, nb, nb, 0.5, seed=41).to(DEV)
+    ops = _ops()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        out, lse = ops.attention_fwd(q, k, v, block_mask=mask, need_lse=True)
+        ref = ops.attention_bwd(do, q, k, v, out, lse, block_mask=mask)
+        sums = []
+        for _ in range(4):
+            dq, dk, dv = ops.attention_bwd(do, q, k, v, out, lse, block_mask=mask)
+            sums.append(dq.float().sum())   # queued on st right behind the call, no sync
+            assert torch.equal(dq, ref[0]) and torch.equal(dk, ref[1]) and torch.equal(dv, ref[2])
+    torch.cuda.synchronize()
+    want = ref[0].float().sum()
+    assert all(torch.equal(s_, want) for s_ in sums)

@@ -32,6 +32,8 @@
 // No atomics: every gradient element is written by exactly one workgroup, so results are
 // bit-reproducible run to run (the reference's deterministic=True).
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "vb_attn_bwd.hpp"
@@ -1025,6 +1027,59 @@ __global__ void __launch_bounds__(256) pool_grad_reduce_kernel(const float* pk, 
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
+#ifndef VB_BWD_FORK
+#define VB_BWD_FORK 1   // D=128: dQ on a side stream beside the dK/dV chain (they share only the prep's output)
+#endif
+// dQ depends only on the prep kernel's row statistics; the dK/dV chain (pooled keys, their reduce,
+// main keys) never reads dQ. So dQ is launched on a per-device side stream that waits for the
+// caller's stream at the fork and is joined back (an event) before the call returns: the two
+// launches fill each other's last rounds and the chain's small launches. Work and results are
+// unchanged (no atomics, disjoint outputs). Graph capture: the side stream joins the caller's
+// capture through the event wait. The mutex keeps one call's record/wait pairs together.
+// Measured (tools/ab.py, profiles/r06_bwd_fork_ab.log): Wan backward 1.016-1.019x, CogVideoX
+// 0.998-1.000x, the multi-level backward 0.987-0.990x, so only the D=128 main backward forks.
+struct BwdFork {
+  hipStream_t side = nullptr;
+  hipEvent_t forked = nullptr, joined = nullptr;
+};
+class ForkScope {
+ public:
+  ForkScope(hipStream_t s, bool enable) : s_(s), lock_(mu()) {
+    if (!VB_BWD_FORK || !enable) return;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    BwdFork& f = forks()[dev];
+    if (!f.side) {
+      if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&f.forked, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&f.joined, hipEventDisableTiming) != hipSuccess) {
+        f = BwdFork{};
+        return;   // no side stream: everything stays on the caller's stream
+      }
+    }
+    if (hipEventRecord(f.forked, s) != hipSuccess || hipStreamWaitEvent(f.side, f.forked, 0) != hipSuccess) return;
+    f_ = &f;
+  }
+  ~ForkScope() {
+    if (f_ && hipEventRecord(f_->joined, f_->side) == hipSuccess) (void)hipStreamWaitEvent(s_, f_->joined, 0);
+  }
+  hipStream_t dq_stream() const { return f_ ? f_->side : s_; }
+  bool forked() const { return f_ != nullptr; }
+
+ private:
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static std::map<int, BwdFork>& forks() {
+    static std::map<int, BwdFork> m;
+    return m;
+  }
+  hipStream_t s_;
+  std::lock_guard<std::mutex> lock_;
+  BwdFork* f_ = nullptr;
+};
+
 template <class T>
 static int launch_prep(const PrepParams& pp, hipStream_t s) {
   const int64_t threads = (int64_t)pp.B * pp.H * pp.ntile * 64 * (pp.D / 8);
@@ -1035,11 +1090,27 @@ static int launch_prep(const PrepParams& pp, hipStream_t s) {
 
 // kernel choice: vb_attn_bwd_args.kernel_select (VB_BWD_SEL_* bits); `ran` collects VB_BWD_RAN_* bits
 template <int D, class T>
+static int launch_dq(const BwdParams& p, bool pool, hipStream_t s, int sel, int& ran) {
+  constexpr bool kF16 = std::is_same<T, F16>::value;
+  if (!(sel & VB_BWD_SEL_DQ_ROUND3)) return launch_dq_pipe(p, D, pool, kF16, s, sel, ran);
+  ran |= VB_BWD_RAN_DQ_ROUND3;
+  const int BH = p.B * p.H;
+  if (pool)
+    hipLaunchKernelGGL((bwd_dq_kernel<D, T, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
+  else
+    hipLaunchKernelGGL((bwd_dq_kernel<D, T, false>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
+  return check_launch("bwd_dq_kernel");
+}
+
+template <int D, class T>
 static int launch_grads(const BwdParams& p, bool pool, hipStream_t s, int sel, int& ran) {
   const int BH = p.B * p.H;
   const bool pipe = !(sel & VB_BWD_SEL_DKDV_ROUND3);
   if ((pool && p.dkp) || p.k) ran |= pipe ? VB_BWD_RAN_DKDV_PIPE : VB_BWD_RAN_DKDV_ROUND3;
   constexpr bool kF16 = std::is_same<T, F16>::value;
+  ForkScope fork(s, D == 128);
+  if (fork.forked())   // dQ first, on the side stream
+    if (int rc = launch_dq<D, T>(p, pool, fork.dq_stream(), sel, ran)) return rc;
   if (pool && p.dkp) {
     if (pipe) {
       if (int rc = launch_dkdv_pipe(p, D, true, kF16, s)) return rc;
@@ -1062,13 +1133,7 @@ static int launch_grads(const BwdParams& p, bool pool, hipStream_t s, int sel, i
       if (int rc = check_launch("bwd_dkdv_kernel")) return rc;
     }
   }
-  if (!(sel & VB_BWD_SEL_DQ_ROUND3)) return launch_dq_pipe(p, D, pool, kF16, s, sel, ran);
-  ran |= VB_BWD_RAN_DQ_ROUND3;
-  if (pool)
-    hipLaunchKernelGGL((bwd_dq_kernel<D, T, true>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
-  else
-    hipLaunchKernelGGL((bwd_dq_kernel<D, T, false>), dim3(p.nbq * BH), dim3(bwd::kThreads), 0, s, p);
-  return check_launch("bwd_dq_kernel");
+  return fork.forked() ? 0 : launch_dq<D, T>(p, pool, s, sel, ran);
 }
 
 static int dispatch_bwd(const PrepParams& pp, const BwdParams& p, int D, int dtype, bool pool, hipStream_t s,
@@ -1331,6 +1396,8 @@ static int launch_ml_grads(const PrepParams& pp, const BwdParams& p, hipStream_t
   if (int rc = launch_prep<T>(pp, s)) return rc;
   ran |= VB_BWD_RAN_ML_PYRAMID;
   const int BH = p.B * p.H;
+  // dQ stays last on the caller's stream: forked beside the pyramid and level-1 passes it measured
+  // 0.987-0.990x (ForkScope)
   {
     constexpr int kW = D == 64 ? VB_ML_PYR_WAVES : 4, kRows = 32 * kW;   // items of kRows pyramid rows
     int items = 0;
