@@ -701,3 +701,30 @@ def test_dispatch_order_small_shapes_batches_and_windows(B, H, L, D, heavy, wind
         keys = [(lin // rows_left, -int(kc[(lin // rows_left) * nb + rows_left - 1 - lin % rows_left]))
                 for lin in seg[skip:]]
         assert keys == sorted(keys), (x, keys)
+
+
+@pytest.mark.parametrize("D,gather,lse", [(64, False, False), (64, True, True), (128, False, True),
+                                          (128, True, False)])
+def test_persistent_fp16_launch_forms(D, gather, lse):
+    """The fp16 instantiations of the persistent forward (each launch form is a separate kernel:
+    head dim, gathered or contiguous K/V, with or without the LSE): the same bits as the
+    one-workgroup-per-q-block launch on ragged batched inputs with a pooled branch, and the queue
+    left zero."""
+    from vblade import ops
+    B, H, L = 2, 3, 900
+    q, k, v = (_rand(B, H, L, D, dtype=torch.float16, seed=s).to(DEV) for s in (60, 61, 62))
+    nb = (L + 127) // 128
+    mask = O.block_mask_from_density(B, H, nb, nb, 0.4, seed=63).to(DEV)
+    rows = torch.randperm(L, generator=torch.Generator().manual_seed(64)).to(torch.int32).to(DEV)
+    kp, vp = (_rand(B, H, 60, D, dtype=torch.float16, seed=s).to(DEV) for s in (65, 66))
+    kw = dict(block_mask=mask, q_rows=rows, kp=kp, vp=vp, kp_log_bias=math.log(15.0), heavy_rows=1,
+              need_lse=lse)
+    if gather:
+        kw["kv_rows"] = rows
+    ref = ops.attention_fwd(q, k, v, **kw)
+    got = ops.attention_fwd(q, k, v, persistent=True, **kw)
+    if lse:
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    else:
+        assert torch.equal(got, ref)
+    assert int(ops.work_queue(q.device).abs().sum()) == 0
