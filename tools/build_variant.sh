@@ -9,7 +9,7 @@ mkdir -p $B "$ROOT/video-blade_amd/vblade/variants"
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$ROOT/include -I$ROOT/video-blade_amd/csrc ${VB_EXTRA_FLAGS}"
 pids=()
 for f in "$ROOT"/video-blade_amd/csrc/*.hip "$ROOT"/video-blade_amd/csrc/*.cpp; do
-  extra=""; case "$f" in *vb_attn_fwd.hip|*vb_attn_fwd_m16.hip) extra="-fno-slp-vectorize -fno-honor-nans ${VB_FWD_FLAGS--mllvm -amdgpu-sched-strategy=iterative-ilp}";; *vb_predict.hip) extra="-fno-honor-nans ${VB_PRED_FLAGS}";; *vb_attn_bwd.hip) extra="${VB_BWD_FLAGS}";; *vb_attn_bwd_kv.hip) extra="-fno-slp-vectorize ${VB_KV_FLAGS}";; esac
+  extra=""; case "$f" in *vb_attn_fwd.hip|*vb_attn_fwd_m16.hip) extra="-fno-slp-vectorize -fno-honor-nans ${VB_FWD_FLAGS--mllvm -amdgpu-sched-strategy=iterative-ilp}";; *vb_predict.hip) extra="-fno-honor-nans ${VB_PRED_FLAGS}";; *vb_attn_bwd.hip) extra="${VB_BWD_FLAGS--mllvm -amdgpu-sched-strategy=iterative-ilp}";; *vb_attn_bwd_kv.hip) extra="-fno-slp-vectorize ${VB_KV_FLAGS}";; esac
   /opt/rocm/bin/hipcc $FL $extra -c "$f" -o $B/$(basename $f).o &
   pids+=($!)
 done
