@@ -1044,8 +1044,9 @@ struct BwdFork {
 };
 class ForkScope {
  public:
-  ForkScope(hipStream_t s, bool enable) : s_(s), lock_(mu()) {
+  ForkScope(hipStream_t s, bool enable) : s_(s), lock_(mu(), std::defer_lock) {
     if (!VB_BWD_FORK || !enable) return;
+    lock_.lock();
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return;
     BwdFork& f = forks()[dev];
@@ -1076,7 +1077,7 @@ class ForkScope {
     return m;
   }
   hipStream_t s_;
-  std::lock_guard<std::mutex> lock_;
+  std::unique_lock<std::mutex> lock_;   // held from the fork to the join (the destructor's event wait)
   BwdFork* f_ = nullptr;
 };
 
