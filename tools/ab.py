@@ -9,9 +9,9 @@ with the multi-level mask as its own vb_level_mask launch (--what mlcall: the mu
 "@win:N" with only the last N q-blocks of each XCD range re-ordered,
 "@env:VAR=VAL+VAR=VAL" with those environment variables set around its launches, "@persist" with the
 persistent (work-queue) attention launch (ops.attention_fwd persistent=True; off otherwise),
-"@sel:N" with the backward's kernel_select bits N (--what bwd / mlbwd). The library latches
-its VB_BWD_* kernel switches once per process (at its first backward call), so A/B a switch with a
-build variant instead (VB_EXTRA_FLAGS=-DVB_BWD_DQ128_DEFAULT=1 tools/build_variant.sh TAG)."""
+"@sel:N" with the backward's kernel_select bits N (--what bwd / mlbwd), "@serialfwd" with the
+training forward's two branches on one stream (--what trainfwd; autograd.FORK_POOLED_BRANCH off).
+Compile-time switches are A/B'd as build variants (VB_EXTRA_FLAGS=-D... tools/build_variant.sh TAG)."""
 import argparse
 import ctypes
 import os
@@ -25,6 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "video-blade_amd"))
 sys.path.insert(0, ROOT)
 import vblade  # noqa: E402
 from vblade import _lib, multilevel, ops  # noqa: E402
+from vblade import autograd as vautograd  # noqa: E402
 from bench import attn_flops, ml_attn_flops, realistic_qkv  # noqa: E402
 
 
@@ -61,6 +62,7 @@ def select(tag, libs):
         if part.startswith("sel:"):
             ORDER[3] = int(part[4:])
     ops.PHILOX_DRAWS = "@torchrand" not in tag
+    vautograd.FORK_POOLED_BRANCH = "@serialfwd" not in tag
     multilevel.FUSED_LEVEL_MASK = "@lvsep" not in tag
     for kv in ENV_SET:
         os.environ.pop(kv, None)
@@ -108,6 +110,10 @@ def main():
             fn = lambda: ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,  # noqa
                                            heavy_rows=m.force_tail, persistent=ORDER[2])[0]
             fl = attn_flops(mask, L, D, 0)
+        elif a.what == "trainfwd":   # the training forward (two LSE branches + combine), no grad taken
+            fn = lambda: vautograd.adaptive_split_attention(q, k, v, mask, rows, m.sample_gap,  # noqa
+                                                            heavy_rows=m.force_tail)
+            fl = attn_flops(mask, L, D, kp.shape[2])
         elif a.what == "pred":
             fn = lambda: m.predict_mask(q, k, qo, ko)  # noqa
         elif a.what == "bwd":   # the training-path backward (vb_attn_bwd) on the two-branch forward
@@ -159,7 +165,7 @@ def main():
                         ref = out[1].clone()
                     else:
                         print(f"  {t}: mask identical to {a.tags[0]}: {torch.equal(out[1], ref)}")
-                if a.what in ("attn", "fwdlse", "bwd", "mlbwd", "mlattn"):
+                if a.what in ("attn", "fwdlse", "bwd", "mlbwd", "mlattn", "trainfwd"):
                     outs = tuple(out) if isinstance(out, tuple) else (out,)   # bwd: dq, dk, dv
                     if ref is None:
                         ref = tuple(o.clone() for o in outs)

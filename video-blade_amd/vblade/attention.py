@@ -47,11 +47,11 @@ VARIANT_DEFAULTS = {
 ORDER_DEFAULT = {"cog": False, "wan": True}
 
 # persistent attention launch (resident-sized grid, per-XCD work queues; ops.attention_fwd
-# persistent=True), per variant. Measured (tools/ab.py, profiles/r06_persist_split_ab.log,
-# r06_persist_unscoped_ab.log): CogVideoX attention 1.005-1.009x; Wan's inference launch (gathered
-# K/V) 0.98x per call, so Wan keeps one workgroup per q-block (its LSE training launch runs
-# persistent: autograd.py).
-PERSISTENT_DEFAULT = {"cog": True, "wan": False}
+# persistent=True), per variant. Measured (tools/ab.py, profiles/r06_persist_*_ab.log): the
+# CogVideoX attention launch alone 1.005-1.009x, but the whole call 0.99-1.00x (r06_persist_call_ab.log);
+# Wan's inference launch (gathered K/V) 0.98x per call. Off for both; the training path's D=128 LSE
+# launch runs persistent (autograd.py, 1.024-1.030x).
+PERSISTENT_DEFAULT = {"cog": False, "wan": False}
 
 
 def retain_counts(nb: int, min_ratio: float, max_ratio: float, variant: str):

@@ -14,6 +14,21 @@ import torch
 
 from . import ops
 
+# The training forward's pooled-only branch (every query against the pooled keys) on a side stream
+# beside the block-sparse branch: the two launches share only their inputs, so they can fill each
+# other's last rounds. Scheduling only: the same bits (tools/ab.py --what trainfwd,
+# profiles/r06_trainfwd_fork_ab.log): Wan (D=128) 1.031-1.034x, CogVideoX 0.989-0.992x, so D=128 only.
+FORK_POOLED_BRANCH = True
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _SIDE_STREAMS.get(idx)
+    if st is None:
+        st = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
+
 
 class _BlockSparseAttnFunc(torch.autograd.Function):
     @staticmethod
@@ -61,10 +76,26 @@ class _AdaptiveSplitFn(torch.autograd.Function):
         kp, vp, k_r, v_r = ops.pool_kv(k, v, gap, rows, reordered=True)
         # the persistent (work-queue) launch at D=128: Wan's LSE forward 1.024-1.030x, CogVideoX's
         # 0.98x (profiles/r06_persist_unscoped_ab.log); bit-identical either way
+        fork = FORK_POOLED_BRANCH and q.is_cuda and q.shape[-1] == 128
+        if fork:
+            cur = torch.cuda.current_stream(q.device)
+            side = _side_stream(q.device)
+            side.wait_stream(cur)   # kp/vp and q are ready
+            with torch.cuda.stream(side):
+                out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp,
+                                               vp=vp, need_lse=True)
+        else:
+            out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
+                                           need_lse=True)
         out1, lse1 = ops.attention_fwd(q, k_r, v_r, block_mask=mask, q_rows=rows, need_lse=True,
                                        heavy_rows=heavy_rows, persistent=q.shape[-1] == 128)
-        out2, lse2 = ops.attention_fwd(q, None, None, use_main=False, q_rows=rows, kp=kp, vp=vp,
-                                       need_lse=True)
+        if fork:
+            cur.wait_stream(side)
+            for t in (q, kp, vp, rows):   # read on the side stream: not reused before it is done
+                if t is not None:
+                    t.record_stream(side)
+            out2.record_stream(cur)
+            lse2.record_stream(cur)
         out, alpha = ops.lse_combine(out1, lse1, out2, lse2, gap)
         ctx.save_for_backward(q, k_r, v_r, mask, rows, out1, lse1, out2, lse2, alpha, kp, vp)
         ctx.gap = gap
