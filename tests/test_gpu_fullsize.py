@@ -9,7 +9,7 @@ with the LSEs cast to bf16 (cogvideo_blocksparseattn.py:324, 374-393). Each case
   ref    the oracle with the reference's rounding (oracle.adaptive_attention),
   exact  the same two branches combined exactly in fp64 (oracle.joint_from_branches),
 and the bounds say which error is whose (tools/diag/quality_decomp.py measures the decomposition,
-including the pre-scaled-Q share; profiles/r03_quality_decomp.json):
+including the pre-scaled-Q share; profiles/archive/r03_quality_decomp.json):
   * PSNR(fused, ref) >= 40 dB (north_star's bar);
   * max|fused - exact| <= 2.5e-2 and >= 99 % of the elements within 2 bf16 ULP of exact: the
     fused path is a faithful bf16 rendering of the exact combine;

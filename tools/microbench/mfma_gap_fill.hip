@@ -2,7 +2,7 @@
 //
 // One 256-thread workgroup per CU (4 waves, one per SIMD), every wave the same loop: per iteration
 // 16 v_mfma_f32_32x32x16_bf16 with a fixed set of fillers pinned after each MFMA by sched_barrier
-// (the structure of the round-4 one-wave-per-SIMD forward experiment, removed from the library in round 5; profiles/r04_fwd1_experiments.md). Modes vary the
+// (the structure of the round-4 one-wave-per-SIMD forward experiment, removed from the library in round 5; profiles/archive/r04_fwd1_experiments.md). Modes vary the
 // accumulator chaining and the filler mix:
 //   acc:   1 = one dependent chain, 2 = two alternating, 4 = four round-robin
 //   fill:  0 = none, 1 = 2 v_exp_f32, 2 = 2 v_add_f32 + 1 v_cvt_pk, 3 = 2 exp + 2 add + 1 pack,

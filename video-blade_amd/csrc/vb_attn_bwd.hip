@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) bwd_prep_kernel(const PrepParams p) {
 #ifndef VB_ML_PYR_WAVES
 // waves per multi-level pooled dK/dV workgroup at D=64: 2 = 64-row items on a 2-slot ring, four
 // workgroups per CU (vb_ml_attn_bwd 1.15x over 4 = 128-row items, dk bit-identical;
-// profiles/r05_ml_bwd_pyr2_ab.log). D=128 keeps 4 (two waves spill there).
+// profiles/archive/r05_ml_bwd_pyr2_ab.log). D=128 keeps 4 (two waves spill there).
 #define VB_ML_PYR_WAVES 2
 #endif
 #ifndef VB_ML_LONG_FIRST

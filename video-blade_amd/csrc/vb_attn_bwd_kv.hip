@@ -32,7 +32,7 @@
 #endif
 #ifndef VB_BWD_DQ128_RING
 // ring slots of the D=128 dQ pipeline: 2 (two workgroups per CU; Wan backward 1.073x over the
-// round-3 dQ, 1.057x over the 4-slot form, profiles/r05_bwd_dq2_ab.log) or 4 (one per CU)
+// round-3 dQ, 1.057x over the 4-slot form, profiles/archive/r05_bwd_dq2_ab.log) or 4 (one per CU)
 #define VB_BWD_DQ128_RING 2
 #endif
 #ifndef VB_DQ2_LA
@@ -40,7 +40,7 @@
 #endif
 #ifndef VB_BWD_DQ64_RING
 // ring slots of the D=64 dQ pipeline: 2 (CogVideoX backward 1.011x over 4, bit-for-bit the same
-// math as the D=128 form; profiles/r05_bwd_dq64_ring_ab.log) or 4
+// math as the D=128 form; profiles/archive/r05_bwd_dq64_ring_ab.log) or 4
 #define VB_BWD_DQ64_RING 2
 #endif
 #ifndef VB_DQ64_R2_WGS

@@ -31,7 +31,7 @@ struct PoolTask {
 #ifndef VB_POOL_NT
 // 1: the K/V reads non-temporal (each row is read once; the score workgroups beside the pass keep
 // more of their L2), 2: the copies' stores too. Per CogVideoX call against the pipelined pass with
-// plain loads: 1.017/1.018x vs 1.015/1.012x, 2: 1.008x (profiles/r05_pool_pipeline_ab.log)
+// plain loads: 1.017/1.018x vs 1.015/1.012x, 2: 1.008x (profiles/archive/r05_pool_pipeline_ab.log)
 #define VB_POOL_NT 1
 #endif
 __device__ __forceinline__ u32x4 pool_ld(const uint8_t* p) {

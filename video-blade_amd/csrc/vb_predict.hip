@@ -74,14 +74,14 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // pooling workgroups after the score workgroups: D=128 (Wan) only. Round 5, with the pipelined pass:
 // Wan call 1.004-1.006x (launch span 246 -> 232 us), CogVideoX 0.945x (its pass outlasts the score
 // kernel's last round); before the pipelining it measured 1-4 % slower on both
-// (profiles/r05_pool_pipeline_ab.log)
+// (profiles/archive/r05_pool_pipeline_ab.log)
 #define VB_FUSED_POOL_LAST 2   // 0: never, 1: both head dims, 2: D=128 only
 #endif
 template <int D> constexpr bool kPoolLast = VB_FUSED_POOL_LAST == 1 || (VB_FUSED_POOL_LAST == 2 && D == 128);
 #ifndef VB_FUSED_POOL_WGS
 // workgroups of the predictor's launch that run the pooled K/V pass (D=128, Wan). Round 5: with the
 // pass pipelined (vb_pool.hpp) 512 measured 0.995x per Wan call against the serial pass, 320 0.999x,
-// 192 0.995x, 128 0.981x (profiles/r05_pool_pipeline_ab.log)
+// 192 0.995x, 128 0.981x (profiles/archive/r05_pool_pipeline_ab.log)
 #define VB_FUSED_POOL_WGS 320
 #endif
 constexpr int kFusedPoolWgs = VB_FUSED_POOL_WGS;

@@ -40,7 +40,7 @@ VARIANT_DEFAULTS = {
 
 
 # longest-first dispatch of the attention launch (one small ordering launch before it), per
-# variant. Measured (tools/ab.py, round 5, profiles/r05_attn_order_ab.log): Wan 1.047-1.054x per
+# variant. Measured (tools/ab.py, round 5, profiles/archive/r05_attn_order_ab.log): Wan 1.047-1.054x per
 # attention launch; CogVideoX 0.98x over the whole range and 0.976-0.989x with only the last
 # 64-256 q-blocks of each XCD range re-ordered (its q-blocks differ little in length, and the
 # Gilbert-neighbour order's L2 reuse and the extra launch cost more than the tail)
