@@ -158,6 +158,8 @@ def main():
         with torch.no_grad():
             for t in a.tags:   # warm + cross-check outputs (a repeated tag checks determinism)
                 select(t, libs)
+                if a.what in ("call", "mlcall"):
+                    torch.cuda.manual_seed(1234)   # the module draws its sampling offsets per call
                 out = fn()
                 torch.cuda.synchronize()
                 if a.what == "pred":   # the same scores and energy rule: masks must be identical
@@ -165,7 +167,7 @@ def main():
                         ref = out[1].clone()
                     else:
                         print(f"  {t}: mask identical to {a.tags[0]}: {torch.equal(out[1], ref)}")
-                if a.what in ("attn", "fwdlse", "bwd", "mlbwd", "mlattn", "trainfwd"):
+                if a.what in ("attn", "fwdlse", "bwd", "mlbwd", "mlattn", "trainfwd", "call", "mlcall"):
                     outs = tuple(out) if isinstance(out, tuple) else (out,)   # bwd: dq, dk, dv
                     if ref is None:
                         ref = tuple(o.clone() for o in outs)
