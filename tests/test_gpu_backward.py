@@ -365,3 +365,33 @@ def test_d128_backward_dq_side_stream_is_joined():
     torch.cuda.synchronize()
     want = ref[0].float().sum()
     assert all(torch.equal(s_, want) for s_ in sums)
+
+
+def test_wan_training_path_forks_are_bit_identical_to_one_stream():
+    """Round 6: at D=128 the training forward runs its pooled-only LSE branch on a side stream
+    (autograd.FORK_POOLED_BRANCH; the backward forks its dQ in both runs, vb_attn_bwd's ForkScope).
+    The module's output and all three gradients equal, bit for bit, those of the one-stream
+    training forward, on a caller-created stream, twice in a row."""
+    from vblade import autograd as va
+    m, _ = _small_module("wan")
+    L = m.gilbert_rearranger.seq_len
+    q, k, v, do = _realistic(1, 2, L, 128, seed=21)
+
+    def run(fork):
+        va.FORK_POOLED_BRANCH = fork
+        qd, kd, vd = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+        torch.cuda.manual_seed(5)
+        out = m(qd, kd, vd)
+        out.backward(do.to(DEV))
+        return out.detach(), qd.grad, kd.grad, vd.grad
+
+    st = torch.cuda.Stream()
+    try:
+        with torch.cuda.stream(st):
+            ref = run(False)
+            got = [run(True) for _ in range(2)]
+        torch.cuda.synchronize()
+    finally:
+        va.FORK_POOLED_BRANCH = True
+    for g in got:
+        assert all(torch.equal(a, b) for a, b in zip(g, ref))
