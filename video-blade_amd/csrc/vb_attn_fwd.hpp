@@ -67,9 +67,10 @@ struct FwdParams {
 #define VB_FWD_PRIO128 3   // measured (Wan, 2 waves per SIMD): 3 +4.1/+4.5 %, 1 +2.5/+5.6 %, 7 +4.2 %, 2 -2.6 %, 4 +0.0 %
 #endif
 // the Q fragment loaded after the ring's first DMAs (their round trips overlap), per launch form.
-// Measured (tools/ab.py, r06, profiles/r06_qlate_ab.log): D=64 attention 1.044-1.048x, its LSE launch
-// 1.058x; D=128 LSE launch 1.047-1.049x, the inference launch on gathered K/V (Wan's module path)
-// 1.001-1.003x per call, on Gilbert copies 0.98x (kept off there)
+// Measured (tools/ab.py, r06, profiles/r06_qlate_ab.log, against the first item-loop build): D=64
+// attention 1.044-1.048x, its LSE launch 1.058x; D=128 LSE launch 1.047-1.049x, the inference launch
+// on gathered K/V (Wan's module path) 1.001-1.003x per call, on Gilbert copies 0.98x (kept off
+// there). On the final tree the CogVideoX call runs 1.002x with it (profiles/r06_fwd_retune_ab.log)
 #ifndef VB_FWD_QLATE64
 #define VB_FWD_QLATE64 1
 #endif
